@@ -1,0 +1,327 @@
+"""Drop-in ``Encoder2Decoder`` for the adaptive-attention model, executed by MI355X HIP kernels.
+
+Mirrors the reference module tree and public surface so callers (``code_src/tools/utils.py:171``
+``model.sampler(images)``, ``code_src/models/model_factory.py:10`` construction,
+``code_src/train.py:177`` state-dict save) work unchanged:
+
+* ``Encoder2Decoder(cf)``             — adaptive_attention.py:159-165
+* ``.sampler(images, max_len=30)``   — adaptive_attention.py:168-216  -> (ids, alpha, beta)
+* ``.encoder(images)``                — AttentiveCNN.forward, baseline_attention.py:36-62
+* ``.decoder(V, v_g, captions, states)`` with one-token captions — Decoder.forward,
+  baseline_attention.py:148-194 (-> scores, alpha, beta, states)
+* state-dict keys identical to the reference (``encoder.affine_a.weight``, ``decoder.LSTM.*``,
+  ``decoder.adaptive.{sentinel,atten,mlp}.*``).
+
+``images`` are the post-trunk ResNet-152 features [B, 2048, 7, 7] (the trunk,
+baseline_attention.py:16-18, is out of scope: ``resnet_conv`` is an empty ``nn.Sequential``).
+Parameters live in ordinary ``nn.Parameter``s; on first use after any change they are packed into
+the kernel layout by ``aa_pack_weights``.  All compute goes through ``libadaptive_amd.so``; there
+is no eager/CPU fallback — a CPU tensor or a missing library raises.
+
+Reference defect D1 (``adaptive_attention.py:183,198`` passes [B,1,H] states to ``nn.LSTM`` and
+raises for B > 1) is not reproduced: the sampler uses the baseline's transpose semantics
+(``baseline_attention.py:251-252``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn import init
+
+from . import _lib
+from .synth import Dims
+
+ATT = 49
+
+
+class Config:
+    """The three ``cf`` attributes the path reads (cfg_wzn.py:115-116, train.py:40)."""
+
+    def __init__(self, adaptive_word_embed_size: int = 256, adaptive_lstm_hidden_size: int = 512,
+                 vocab_length: int = 10123):
+        self.adaptive_word_embed_size = adaptive_word_embed_size
+        self.adaptive_lstm_hidden_size = adaptive_lstm_hidden_size
+        self.vocab_length = vocab_length
+
+
+# ---- reference-style initialisers (model_utils.py:4-74) ------------------------------------------
+def _xavier_uniform(nonlinearity, *mods):
+    gain = init.calculate_gain(nonlinearity)
+    for m in mods:
+        init.xavier_uniform_(m.weight, gain)
+        if m.bias is not None:
+            m.bias.data.fill_(0)
+
+
+def _kaiming(fn, nonlinearity, a, *mods):
+    for m in mods:
+        fn(m.weight, a=a, mode="fan_in", nonlinearity=nonlinearity)
+        if m.bias is not None:
+            m.bias.data.fill_(0)
+
+
+def _lstm_init(lstm: nn.LSTM):
+    H = lstm.hidden_size
+    for name, p in lstm.named_parameters():
+        if "bias" in name:
+            init.constant_(p, 0.0)
+            p.data[H:2 * H] = 0.5
+        elif "weight" in name:
+            init.orthogonal_(p)
+
+
+class AttentiveCNN(nn.Module):
+    """Encoder tail (baseline_attention.py:11-62) over post-trunk features."""
+
+    def __init__(self, embed_size: int, hidden_size: int, cf=None, channels: int = 2048):
+        super().__init__()
+        self.resnet_conv = nn.Sequential()  # trunk out of scope; identity over [B,2048,7,7]
+        self.avgpool = nn.AvgPool2d(7)
+        self.affine_a = nn.Linear(channels, hidden_size)
+        self.affine_b = nn.Linear(channels, embed_size)
+        self.dropout = nn.Dropout(0)
+        _kaiming(init.kaiming_uniform_, "relu", 0, self.affine_a, self.affine_b)
+        self.affine_h0 = nn.Linear(channels, hidden_size)
+        self.affine_c0 = nn.Linear(channels, hidden_size)
+        _xavier_uniform("tanh", self.affine_h0, self.affine_c0)
+        self._owner = None  # set by Encoder2Decoder (weak back-reference for packing)
+
+    def forward(self, images: torch.Tensor):
+        """-> V [B,49,H], v_g [B,E], (h0, c0) each [B,1,H] (baseline_attention.py:43-62)."""
+        owner = self._owner
+        if owner is None:
+            raise RuntimeError("AttentiveCNN must be used through Encoder2Decoder (it owns the packed weights)")
+        return owner._encode(images)[:3]
+
+
+class Atten(nn.Module):
+    """Parameter holder of adaptive_attention.py:12-24."""
+
+    def __init__(self, hidden_size: int, cf=None):
+        super().__init__()
+        self.affine_v = nn.Linear(hidden_size, ATT, bias=False)
+        self.affine_g = nn.Linear(hidden_size, ATT, bias=False)
+        self.affine_s = nn.Linear(hidden_size, ATT, bias=False)
+        self.affine_h = nn.Linear(ATT, 1, bias=False)
+        self.dropout = nn.Dropout(0)
+        _xavier_uniform("tanh", self.affine_v, self.affine_g, self.affine_s)
+        _kaiming(init.kaiming_normal_, "relu", 0, self.affine_h)
+
+
+class Sentinel(nn.Module):
+    """Parameter holder of adaptive_attention.py:62-73."""
+
+    def __init__(self, input_size: int, hidden_size: int):
+        super().__init__()
+        self.affine_x = nn.Linear(input_size, hidden_size, bias=False)
+        self.affine_h = nn.Linear(hidden_size, hidden_size, bias=False)
+        self.dropout = nn.Dropout(0)
+        _xavier_uniform("sigmoid", self.affine_x, self.affine_h)
+
+
+class AdaptiveBlock(nn.Module):
+    """Parameter holder of adaptive_attention.py:89-108."""
+
+    def __init__(self, embed_size: int, hidden_size: int, vocab_size: int, cf=None):
+        super().__init__()
+        self.sentinel = Sentinel(embed_size * 2, hidden_size)
+        self.atten = Atten(hidden_size, cf)
+        self.mlp = nn.Linear(hidden_size, vocab_size)
+        self.dropout = nn.Dropout(0)
+        self.hidden_size = hidden_size
+        _kaiming(init.kaiming_normal_, "relu", 0, self.mlp)
+
+
+class Decoder(nn.Module):
+    """Decoder (baseline_attention.py:132-194 + adaptive_attention.py:151-155)."""
+
+    def __init__(self, embed_size: int, vocab_size: int, hidden_size: int, cf=None):
+        super().__init__()
+        self.embed = nn.Embedding(vocab_size, embed_size)
+        self.LSTM = nn.LSTM(embed_size * 2, hidden_size, 1, batch_first=True)
+        self.adaptive = AdaptiveBlock(embed_size, hidden_size, vocab_size, cf)
+        _lstm_init(self.LSTM)
+        self._owner = None
+
+    def forward(self, V, v_g, captions, states=None):
+        owner = self._owner
+        if owner is None:
+            raise RuntimeError("Decoder must be used through Encoder2Decoder (it owns the packed weights)")
+        return owner._decode_step(V, v_g, captions, states)
+
+
+class Encoder2Decoder(nn.Module):
+    """adaptive_attention.Encoder2Decoder on MI355X kernels."""
+
+    def __init__(self, cf):
+        nn.Module.__init__(self)
+        E, H, V = cf.adaptive_word_embed_size, cf.adaptive_lstm_hidden_size, cf.vocab_length
+        self.encoder = AttentiveCNN(E, H, cf)
+        self.decoder = Decoder(E, V, H, cf)
+        object.__setattr__(self.encoder, "_owner", self)
+        object.__setattr__(self.decoder, "_owner", self)
+        self.dims = Dims(embed=E, hidden=H, vocab=V)
+        self._pack_key = None
+        self._packed = None
+        self._model = None
+
+    # ---- weights -------------------------------------------------------------------------------
+    def load_synthetic(self, seed: int = 123, bias_noise: float = 0.0) -> "Encoder2Decoder":
+        """Load the counter-based synthetic weights (adaptive_amd.synth) — identical on every host."""
+        from .synth import make_weights
+        sd = make_weights(seed, self.dims, bias_noise=bias_noise)
+        dev = next(self.parameters()).device
+        self.load_state_dict({k: torch.from_numpy(v).to(dev) for k, v in sd.items()}, strict=True)
+        return self
+
+    def load_state_dict(self, state_dict, strict: bool = True, **kw):
+        # a real checkpoint (train.py:177) also carries the ResNet trunk under encoder.resnet_conv.*;
+        # the trunk is out of scope here, so those keys are dropped.
+        sd = {k: v for k, v in state_dict.items() if not k.startswith("encoder.resnet_conv.")}
+        return super().load_state_dict(sd, strict=strict, **kw)
+
+    def _c_dims(self) -> _lib.Dims:
+        d = self.dims
+        return _lib.Dims(d.embed, d.hidden, d.vocab, d.channels, d.spatial)
+
+    def _model_struct(self) -> _lib.Model:
+        """Pack parameters if any changed since the last pack (data_ptr + version counters)."""
+        params = dict(self.named_parameters())
+        names = [k for _, k in _lib.WEIGHT_FIELDS]
+        dev = params[names[0]].device
+        if dev.type != "cuda":
+            raise RuntimeError("adaptive_amd.Encoder2Decoder runs on the GPU only: call .cuda() first")
+        key = tuple((params[n].data_ptr(), params[n]._version) for n in names)
+        if key == self._pack_key and self._model is not None:
+            return self._model
+        lib = _lib.load()
+        cd = self._c_dims()
+        _lib.check(lib.aa_check_dims(cd), "dims")
+        nbytes = lib.aa_packed_bytes(cd)
+        for n in names:
+            p = params[n]
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev:
+                raise RuntimeError(f"adaptive_amd: parameter {n} must be contiguous fp32 on {dev}")
+        packed = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        model = _lib.Model(cd, packed.data_ptr(), nbytes)
+        w = _lib.RefWeights(**{f: params[k].data_ptr() for f, k in _lib.WEIGHT_FIELDS})
+        with torch.cuda.device(dev):
+            _lib.check(lib.aa_pack_weights(model, w, _lib.stream_handle()), "pack_weights")
+        self._packed, self._model, self._pack_key = packed, model, key
+        return model
+
+    def _check_images(self, images: torch.Tensor) -> torch.Tensor:
+        d = self.dims
+        if images.dim() != 4 or tuple(images.shape[1:]) != (d.channels, 7, 7):
+            raise ValueError(f"images must be post-trunk features [B,{d.channels},7,7], got {tuple(images.shape)}")
+        if not images.is_cuda:
+            raise RuntimeError("adaptive_amd: images must be a CUDA (ROCm) tensor")
+        if images.dtype != torch.float32:
+            raise TypeError("adaptive_amd: images must be float32")
+        return images.contiguous()
+
+    # ---- Encoder2Decoder.sampler (adaptive_attention.py:168-216) --------------------------------
+    @torch.no_grad()
+    def sampler(self, images: torch.Tensor, max_len: int = 30, trace: Optional[_lib.Trace] = None):
+        """Greedy decode -> (ids [B,max_len] int64, alpha [B,max_len,49], beta [B,max_len,1])."""
+        images = self._check_images(images)
+        model = self._model_struct()
+        lib = _lib.load()
+        B, T, dev = images.size(0), int(max_len), images.device
+        ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+        alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+        beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+        ws = self._workspace(lib.aa_decode_workspace_bytes(self._c_dims(), B, T), dev)
+        with torch.cuda.device(dev):
+            rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                      beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                                      trace, _lib.stream_handle())
+        _lib.check(rc, "greedy_decode")
+        return ids, alpha, beta
+
+    def _workspace(self, nbytes: int, dev) -> Optional[torch.Tensor]:
+        if nbytes == 0:
+            return None
+        ws = getattr(self, "_ws", None)
+        if ws is None or ws.numel() < nbytes or ws.device != dev:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            self._ws = ws
+        return ws
+
+    # ---- AttentiveCNN.forward (baseline_attention.py:36-62) -------------------------------------
+    @torch.no_grad()
+    def _encode(self, images: torch.Tensor):
+        images = self._check_images(images)
+        model = self._model_struct()
+        lib = _lib.load()
+        d, B, dev = self.dims, images.size(0), images.device
+        a_g = torch.empty(B, d.channels, device=dev)
+        V = torch.empty(B, ATT, d.hidden, device=dev)
+        v_g = torch.empty(B, d.embed, device=dev)
+        h0 = torch.empty(B, 1, d.hidden, device=dev)
+        c0 = torch.empty(B, 1, d.hidden, device=dev)
+        VWv = torch.empty(B, ATT, 64, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.aa_encoder_tail(model, images.data_ptr(), B, a_g.data_ptr(), V.data_ptr(), v_g.data_ptr(),
+                                     h0.data_ptr(), c0.data_ptr(), VWv.data_ptr(), _lib.stream_handle())
+        _lib.check(rc, "encoder_tail")
+        return V, v_g, (h0, c0), a_g, VWv
+
+    # ---- Decoder.forward with one-token captions (baseline_attention.py:148-194) -----------------
+    @torch.no_grad()
+    def _decode_step(self, V, v_g, captions, states):
+        d = self.dims
+        if captions.dim() != 2 or captions.size(1) != 1:
+            raise NotImplementedError(
+                "adaptive_amd: Decoder.forward is implemented for one-token steps (sampling). Teacher-forced "
+                "multi-step decoding (training, SURVEY.md §8f row 1) is not built yet.")
+        B, dev = V.size(0), V.device
+        if states is None:
+            raise ValueError("states (h, c) are required")
+        h, c = states
+        # accept [1,B,H] (LSTM layout) or [B,1,H] (encoder output layout)
+        h = h.reshape(B, d.hidden).contiguous()
+        c = c.reshape(B, d.hidden).contiguous()
+        tokens = captions.reshape(B).to(torch.int64).contiguous()
+        if B and (int(tokens.min()) < 0 or int(tokens.max()) >= d.vocab):
+            raise IndexError("index out of range in self (embedding)")  # nn.Embedding's error
+        model = self._model_struct()
+        lib = _lib.load()
+        V = V.contiguous()
+        v_g = v_g.contiguous()
+        h_out = torch.empty(1, B, d.hidden, device=dev)
+        c_out = torch.empty(1, B, d.hidden, device=dev)
+        scores = torch.empty(B, 1, d.vocab, device=dev)
+        tok_out = torch.empty(B, dtype=torch.int64, device=dev)
+        alpha = torch.empty(B, 1, ATT, device=dev)
+        beta = torch.empty(B, 1, 1, device=dev)
+        ws = self._workspace(lib.aa_step_workspace_bytes(self._c_dims(), B), dev)
+        with torch.cuda.device(dev):
+            rc = lib.aa_decode_step(model, B, tokens.data_ptr(), V.data_ptr(), None, v_g.data_ptr(), h.data_ptr(),
+                                    c.data_ptr(), h_out.data_ptr(), c_out.data_ptr(), scores.data_ptr(),
+                                    tok_out.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
+                                    ws.numel() if ws is not None else 0, _lib.stream_handle())
+        _lib.check(rc, "decode_step")
+        self._last_tokens = tok_out
+        return scores, alpha, beta, (h_out, c_out)
+
+    def forward(self, images, captions, lengths):
+        raise NotImplementedError(
+            "adaptive_amd: teacher-forced Encoder2Decoder.forward (training, baseline_attention.py:206-230) is "
+            "SURVEY.md §8f row 1 and not built yet; use sampler() for decoding.")
+
+
+def synthetic_features(B: int, device, seed: int = 0, row0: int = 0, dims: Dims = Dims()) -> torch.Tensor:
+    """[B, C, 7, 7] U[0,1) features generated ON the GPU by aa_synth_uniform (same bits as
+    adaptive_amd.synth.make_features)."""
+    from .synth import stream_key
+    lib = _lib.load()
+    per_row = dims.channels * dims.spatial
+    out = torch.empty(B, dims.channels, 7, 7, dtype=torch.float32, device=device)
+    with torch.cuda.device(out.device):
+        _lib.check(lib.aa_synth_uniform(out.data_ptr(), B * per_row, stream_key(seed, "features"), row0 * per_row,
+                                        0.0, 1.0, _lib.stream_handle()), "synth_uniform")
+    return out

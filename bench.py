@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: greedy adaptive-attention decode (Encoder2Decoder.sampler, max_len=20) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 512] [--max-len 20]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+A "step" = one sampler() call over this rank's B = 512 synthetic images (post-trunk features
+[B,2048,7,7], U[0,1), counter-based; random-init weights of the reference architecture, seed 123)
+plus, for N > 1, the RCCL all-gather of the token ids (the path's only collective).  Each rank
+decodes its own rows (weak scaling: global batch = 512 N).  Inputs are resident in HBM before the
+timed region.  Rank 0 prints ONE JSON line.
+
+Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic FLOPs / its average
+HIP-event duration inside the timed region), ``kernels`` (all per-kernel averages),
+``path_roofline`` (whole decode vs the fp32 MFMA peak), ``cpu_baseline`` (the PyTorch-CPU
+restatement of the reference sampler, oracle/adaptive_oracle.py, timed on this host, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
+from adaptive_amd import _lib  # noqa: E402
+from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
+from adaptive_amd.hip_events import EventArray  # noqa: E402
+
+METRIC = "captions/sec (greedy, max_len=20) at B=512; 1/2/4/8-GPU scaling"
+PEAK_FP32 = 157.3e12     # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
+PEAK_HBM = 8.0e12        # HBM3E spec
+E, H, V, C, P = 256, 512, 10123, 2048, 49
+
+
+def flops_per_caption(T: int) -> dict:
+    """Algorithmic FLOPs: no redundant ops, transcendentals excluded."""
+    enc = 2 * P * C * H + 2 * C * E + 2 * 2 * C * H + P * C
+    vwv = 2 * P * H * P
+    lstm = 2 * (2 * E + H) * 4 * H + 2 * (2 * E) * H          # gates GEMM + sentinel x-term
+    atten = 2 * 2 * H * P + 2 * P * P + 2 * P + 2 * P * H       # W_g h, W_s s; scores; context
+    vocab = 2 * H * V
+    return {"encoder": enc + vwv, "lstm": lstm, "atten": atten, "vocab": vocab,
+            "total": enc + vwv + T * (lstm + atten + vocab)}
+
+
+def atten_bytes_per_row() -> int:
+    """k_atten algorithmic HBM bytes per row: V rows + VWv rows + h, c, sx in, u out, alpha/beta out."""
+    return 4 * (P * H + P * P + 3 * H + H + P + 1)
+
+
+def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
+    from oracle.adaptive_oracle import OracleModel  # test/baseline infrastructure only
+    threads = int(os.environ.get("AA_CPU_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    m = OracleModel(synth.make_weights(123))
+    m.sampler(feats_cpu[:8], max_len=2)  # warm-up
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 5):
+        t0 = time.perf_counter()
+        m.sampler(feats_cpu, max_len=T)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    B = feats_cpu.size(0)
+    return {"value": B / med, "unit": "captions/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/adaptive_oracle.py sampler (PyTorch-CPU fp32 restatement of the reference, "
+                      f"reference op order) on the same B={B}, max_len={T} batch; median of {len(times)} runs "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s); {threads} threads; {cpu_model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512, help="images per GPU")
+    ap.add_argument("--max-len", type=int, default=20)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit(f"--gpus {args.gpus} needs a torchrun launch with {args.gpus} processes")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, T = args.batch, args.max_len
+    model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    feats = synthetic_features(B, dev, seed=0, row0=rank * B)  # rows [rank*B, (rank+1)*B) of the global batch
+    ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
+
+    def step(trace=None):
+        ids, alpha, beta = model.sampler(feats, max_len=T, trace=trace)
+        if world > 1:
+            dist.all_gather_into_tensor(ids_all, ids)
+        return ids
+
+    for _ in range(args.warmup):
+        step()
+    K = args.steps
+    traces = []
+    if not args.no_trace:
+        for _ in range(K):
+            ev = {k: EventArray(2 * T) for k in ("vocab", "lstm", "atten")}
+            ev["encoder"] = EventArray(2)
+            tr = _lib.Trace(ev["vocab"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["encoder"].ptr)
+            traces.append((ev, tr))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(traces[k][1] if traces else None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    captions = world * B * K
+    value = captions / elapsed
+    ms_per_step = 1e3 * elapsed / K
+
+    fl = flops_per_caption(T)
+    kernels = {}
+    if traces:
+        per = {k: [] for k in ("vocab", "lstm", "atten", "encoder")}
+        for ev, _ in traces:
+            for k in per:
+                per[k] += ev[k].pair_durations_ms()
+        for k, ds in per.items():
+            avg_ms = float(np.mean(ds))
+            launches_per_step = 1 if k == "encoder" else T
+            entry = {"avg_ms": avg_ms, "launches": len(ds), "share_of_step": avg_ms * launches_per_step / ms_per_step}
+            if k == "atten":
+                byt = atten_bytes_per_row() * B
+                entry.update({"bound": "hbm", "achieved": byt / (avg_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
+                              "unit": "GB/s", "algorithmic_bytes_per_launch": byt})
+            else:
+                f = fl[k] * B
+                entry.update({"bound": "mfma", "achieved": f / (avg_ms * 1e-3) / 1e12, "peak": PEAK_FP32 / 1e12,
+                              "unit": "TFLOP/s", "algorithmic_flops_per_launch": f})
+            entry["frac"] = entry["achieved"] / entry["peak"]
+            kernels[k] = entry
+    dominant = max(kernels, key=lambda k: kernels[k]["share_of_step"]) if kernels else None
+    roofline = None
+    if dominant:
+        kd = kernels[dominant]
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get(dominant, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
+                    "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic}
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: counter-based U[0,1) post-trunk features [B,2048,7,7] and synthetic random-init "
+                "weights of the reference architecture (adaptive_amd/synth.py, seed 123)",
+        "config": {"workload": f"greedy decode (Encoder2Decoder.sampler) B={B}/GPU, max_len={T}",
+                   "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
+                   "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else "")},
+        "roofline": roofline,
+        "path_roofline": {"bound": "mfma", "achieved": fl["total"] * value / 1e12, "peak": PEAK_FP32 / 1e12,
+                          "unit": "TFLOP/s", "frac": fl["total"] * value / PEAK_FP32,
+                          "flops_per_caption": fl["total"]},
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(feats.cpu(), T, args.cpu_budget)
+        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

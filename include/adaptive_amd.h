@@ -1,0 +1,157 @@
+/*
+ * adaptive_amd.h — C-ABI of the MI355X-native adaptive-attention ("Knowing When to Look")
+ * greedy-decode path.  Plain C: device pointers, sizes, opaque stream/event handles.
+ *
+ * The reference has no FFI: its boundary is the Python module API of
+ *   code_src/models/adaptive_attention.py:159-216  (Encoder2Decoder, .sampler)
+ *   code_src/models/baseline_attention.py:36-62    (AttentiveCNN.forward, the encoder tail)
+ *   code_src/models/baseline_attention.py:148-194  (Decoder.forward, one step when T == 1)
+ * Each entry point below names the reference interface it replaces.  The Python host layer
+ * (adaptive_amd/adaptive_attention.py) binds them with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - All tensors are fp32 (ids int64), contiguous, row-major, caller-owned DEVICE memory.
+ *  - No call allocates memory or synchronises the stream; scratch comes from a caller-provided
+ *    workspace whose size is returned by the *_workspace_bytes queries.  Every launch goes to
+ *    the given stream, so a caller may capture a call into a hipGraph.
+ *  - Return value: 0 = success; negative = argument/shape error (see AA_ERR_*); positive = the
+ *    hipError_t of a failed HIP call.  Nothing throws across the ABI.
+ *  - Stateless and re-entrant: no hidden globals.
+ *  - Load the library only after the process's HIP runtime is loaded (e.g. after `import torch`)
+ *    so that one libamdhip64.so.7 serves both.
+ */
+#ifndef ADAPTIVE_AMD_H
+#define ADAPTIVE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AA_ABI_VERSION 1
+#define AA_API __attribute__((visibility("default")))
+
+/* error codes (negative); positive codes are hipError_t values */
+#define AA_OK 0
+#define AA_ERR_NULL (-1)      /* a required pointer is NULL */
+#define AA_ERR_DIMS (-2)      /* unsupported model dimensions */
+#define AA_ERR_SHAPE (-3)     /* bad batch size / step count */
+#define AA_ERR_BUFFER (-4)    /* packed-weight or workspace buffer too small */
+#define AA_ERR_ALIGN (-5)     /* a pointer is not 16-byte aligned */
+
+typedef void* aa_stream_t; /* hipStream_t (NULL = legacy default stream) */
+typedef void* aa_event_t;  /* hipEvent_t */
+
+/* Model dimensions: cf.adaptive_word_embed_size, cf.adaptive_lstm_hidden_size, cf.vocab_length
+ * (code_src/config/cfg_wzn.py:115-116, code_src/train.py:40), ResNet channels and 7x7 locations.
+ * Supported: embed % 32 == 0, hidden % 128 == 0 and <= 1024, vocab >= 1, channels % 32 == 0,
+ * spatial == 49. */
+typedef struct aa_dims {
+  int32_t embed;    /* E = 256 */
+  int32_t hidden;   /* H = 512 */
+  int32_t vocab;    /* V = 10123 */
+  int32_t channels; /* C = 2048 */
+  int32_t spatial;  /* P = 49 */
+} aa_dims;
+
+/* Parameters in the reference state-dict layout (device pointers, fp32, contiguous).
+ * Names follow Encoder2Decoder.state_dict() keys. */
+typedef struct aa_ref_weights {
+  const float* enc_affine_a_w;  /* encoder.affine_a.weight  [H, C] */
+  const float* enc_affine_a_b;  /* encoder.affine_a.bias    [H]    */
+  const float* enc_affine_b_w;  /* encoder.affine_b.weight  [E, C] */
+  const float* enc_affine_b_b;  /* encoder.affine_b.bias    [E]    */
+  const float* enc_affine_h0_w; /* encoder.affine_h0.weight [H, C] */
+  const float* enc_affine_h0_b; /* encoder.affine_h0.bias   [H]    */
+  const float* enc_affine_c0_w; /* encoder.affine_c0.weight [H, C] */
+  const float* enc_affine_c0_b; /* encoder.affine_c0.bias   [H]    */
+  const float* embed_w;         /* decoder.embed.weight     [V, E] */
+  const float* lstm_w_ih;       /* decoder.LSTM.weight_ih_l0 [4H, 2E] (gates i,f,g,o) */
+  const float* lstm_w_hh;       /* decoder.LSTM.weight_hh_l0 [4H, H]  */
+  const float* lstm_b_ih;       /* decoder.LSTM.bias_ih_l0   [4H]     */
+  const float* lstm_b_hh;       /* decoder.LSTM.bias_hh_l0   [4H]     */
+  const float* sent_affine_x_w; /* decoder.adaptive.sentinel.affine_x.weight [H, 2E] */
+  const float* sent_affine_h_w; /* decoder.adaptive.sentinel.affine_h.weight [H, H]
+                                   (multiplies h_{t-1} = 0 while sampling; may be NULL) */
+  const float* att_affine_v_w;  /* decoder.adaptive.atten.affine_v.weight [P, H] */
+  const float* att_affine_g_w;  /* decoder.adaptive.atten.affine_g.weight [P, H] */
+  const float* att_affine_s_w;  /* decoder.adaptive.atten.affine_s.weight [P, H] */
+  const float* att_affine_h_w;  /* decoder.adaptive.atten.affine_h.weight [1, P] */
+  const float* mlp_w;           /* decoder.adaptive.mlp.weight [V, H] */
+  const float* mlp_b;           /* decoder.adaptive.mlp.bias   [V]    */
+} aa_ref_weights;
+
+/* A model = dims + a caller-owned device buffer holding the packed (kernel-layout) weights. */
+typedef struct aa_model {
+  aa_dims dims;
+  void* packed;        /* device buffer, >= aa_packed_bytes(&dims) bytes, 256-B aligned */
+  size_t packed_bytes;
+} aa_model;
+
+/* Optional per-kernel timing (hipEvent_t handles created by the caller).  For each non-NULL array,
+ * aa_greedy_decode records event [2t] before and [2t+1] after the corresponding launch of step t
+ * (2*T events each); encoder_events gets 2 events around the encoder tail. */
+typedef struct aa_trace {
+  aa_event_t* vocab_events;
+  aa_event_t* lstm_events;
+  aa_event_t* atten_events;
+  aa_event_t* encoder_events; /* 2 events around the encoder tail (may be NULL) */
+} aa_trace;
+
+AA_API int aa_abi_version(void);
+AA_API const char* aa_error_string(int code);
+AA_API int aa_check_dims(const aa_dims* dims);
+
+/* Bytes of the packed weight buffer for these dims. */
+AA_API size_t aa_packed_bytes(const aa_dims* dims);
+
+/* Pack reference-layout weights into m->packed (device-side reorder; async on `stream`).
+ * Replaces: the parameter set built by Encoder2Decoder.__init__ / load_state_dict
+ * (adaptive_attention.py:159-165, model_factory.py:16). */
+AA_API int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stream);
+
+/* Encoder tail: a_g = AvgPool2d(7)(A); V = relu(A^T W_a^T + b_a); v_g = relu(a_g W_b^T + b_b);
+ * h0/c0 = tanh(a_g W^T + b); plus the step-invariant VWv = V W_v^T used by every decode step.
+ * Replaces AttentiveCNN.forward after resnet_conv (baseline_attention.py:46-62).
+ * feats: [B, C, 7, 7] NCHW post-trunk features.  Outputs: a_g [B,C], V [B,P,H], v_g [B,E],
+ * h0 [B,H], c0 [B,H], VWv [B,P,64] (columns >= P are zero; may be NULL). */
+AA_API int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g, float* V,
+                           float* v_g, float* h0, float* c0, float* VWv, aa_stream_t stream);
+
+/* Workspace for aa_decode_step at batch B. */
+AA_API size_t aa_step_workspace_bytes(const aa_dims* dims, int32_t B);
+
+/* One greedy decode step = Decoder.forward with T == 1 (baseline_attention.py:148-194) through
+ * AdaptiveBlock (adaptive_attention.py:110-134) and the argmax of Encoder2Decoder.sampler (:201).
+ * tokens_in [B] int64 (NULL = <start> = 1); VWv from aa_encoder_tail (may be NULL: recomputed);
+ * h_in/c_in [B,H] -> h_out/c_out [B,H]; scores [B,V] (NULL = not written); tokens_out [B] int64
+ * (first index on ties); alpha [B,P]; beta [B].  h_out/c_out must not alias h_in/c_in. */
+AA_API int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const float* V,
+                          const float* VWv, const float* v_g, const float* h_in, const float* c_in,
+                          float* h_out, float* c_out, float* scores, int64_t* tokens_out,
+                          float* alpha, float* beta, void* workspace, size_t workspace_bytes,
+                          aa_stream_t stream);
+
+/* Workspace for aa_greedy_decode at batch B and T steps. */
+AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
+
+/* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
+ * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];
+ * ids [B,T] int64; alpha [B,T,P] and beta [B,T] may be NULL.  All T steps run (no early stop),
+ * the first input token is <start> = 1.  trace may be NULL. */
+AA_API int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T,
+                            int64_t* ids, float* alpha, float* beta, void* workspace,
+                            size_t workspace_bytes, const aa_trace* trace, aa_stream_t stream);
+
+/* Counter-based synthetic data (same bits as adaptive_amd/synth.py):
+ * dst[i] = fp32(lo + (hi - lo) * u(key, start + i)), u = (splitmix64(key + (start+i+1)*GOLDEN) >> 40) / 2^24.
+ * For lo = 0, hi = 1 the value is u exactly. */
+AA_API int aa_synth_uniform(float* dst, int64_t n, uint64_t key, int64_t start, double lo,
+                            double hi, aa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADAPTIVE_AMD_H */

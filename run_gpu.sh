@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU-box driver: every GPU step under its own timeout; stop at the first crash/timeout.
+# usage: bash run_gpu.sh <step>...   steps: smoke tests bench prof
+set -u
+mkdir -p gpurun_out
+ok_or_fail() {  # continue on 0 (pass) or 1 (test failures); stop on crashes/timeouts
+  local rc=$1 name=$2
+  echo "[$name] exit $rc"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "[$name] crashed/timed out -> stopping"; exit "$rc"; fi
+}
+for step in "$@"; do
+  case "$step" in
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok_or_fail $? smoke; tail -3 gpurun_out/smoke.log ;;
+    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -15 gpurun_out/pytest_gpu.log ;;
+    testsall) timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -25 gpurun_out/pytest_gpu.log ;;
+    bench) timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
+    benchq) timeout -k 10 600 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-trace --steps 10 > gpurun_out/prof.log 2>&1; ok_or_fail $? prof ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,189 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the reference goldens.
+
+Tolerances (fp32 end to end on both sides; the two differ only in summation order and libm ulps):
+* token ids: bit-identical (the north-star bar);
+* logits: |GPU - oracle| <= 1e-4 (north-star), typically ~1e-6;
+* alpha / beta / encoder outputs: <= 2e-5 absolute.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+from adaptive_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-4
+ATT_TOL = 2e-5
+
+
+def _model(seed=123, bias_noise=0.0, dev="cuda:0"):
+    from adaptive_amd import Config, Encoder2Decoder
+    m = Encoder2Decoder(Config()).to(dev)
+    m.load_synthetic(seed, bias_noise=bias_noise)
+    return m
+
+
+def _oracle(seed=123, bias_noise=0.0):
+    from oracle.adaptive_oracle import OracleModel
+    return OracleModel(synth.make_weights(seed, bias_noise=bias_noise))
+
+
+@pytest.fixture(scope="module")
+def model(gpu_device):
+    return _model()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return _oracle()
+
+
+def test_synth_features_bit_exact(gpu_device):
+    from adaptive_amd.adaptive_attention import synthetic_features
+    for B, row0 in [(2, 0), (3, 5)]:
+        g = synthetic_features(B, gpu_device, seed=0, row0=row0).cpu().numpy()
+        c = synth.make_features(B, seed=0, row0=row0)
+        assert np.array_equal(g.view(np.uint32), c.view(np.uint32))
+
+
+def test_encoder_tail(model, oracle, gpu_device):
+    B = 5
+    feats = synth.make_features(B)
+    V, v_g, (h0, c0), a_g, VWv = model._encode(torch.from_numpy(feats).to(gpu_device))
+    rV, rvg, (rh0, rc0), ra_g = oracle.encoder(torch.from_numpy(feats))
+    assert np.array_equal(a_g.cpu().numpy(), ra_g.numpy()), "avg-pool must be bit-exact (sequential fp32 sum)"
+    np.testing.assert_allclose(V.cpu().numpy(), rV.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(v_g.cpu().numpy(), rvg.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(h0.cpu().numpy()[:, 0], rh0.numpy()[0], atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(c0.cpu().numpy()[:, 0], rc0.numpy()[0], atol=ATT_TOL, rtol=0)
+    Wv = oracle.w["decoder.adaptive.atten.affine_v.weight"]
+    ref_vwv = torch.nn.functional.linear(rV, Wv).numpy()
+    got = VWv.cpu().numpy()
+    np.testing.assert_allclose(got[..., :49], ref_vwv, atol=ATT_TOL, rtol=0)
+    assert np.all(got[..., 49:] == 0)
+
+
+def test_decode_step_logits(model, oracle, gpu_device):
+    """One Decoder.forward step (T == 1) from the encoder states: logits within 1e-4."""
+    B = 7
+    feats = torch.from_numpy(synth.make_features(B, seed=3))
+    rV, rvg, rstates, _ = oracle.encoder(feats)
+    caps = torch.full((B, 1), 1, dtype=torch.int64)
+    r_scores, r_alpha, r_beta, r_states = oracle.decoder(rV, rvg, caps, rstates)
+    V, v_g, (h0, c0), _, _ = model._encode(feats.to(gpu_device))
+    scores, alpha, beta, (h1, c1) = model.decoder(V, v_g, caps.to(gpu_device), (h0, c0))
+    np.testing.assert_allclose(scores.cpu().numpy(), r_scores.numpy(), atol=LOGIT_TOL, rtol=0)
+    np.testing.assert_allclose(alpha.cpu().numpy(), r_alpha.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(beta.cpu().numpy(), r_beta.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(h1.cpu().numpy(), r_states[0].numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(c1.cpu().numpy(), r_states[1].numpy(), atol=ATT_TOL, rtol=0)
+    assert torch.equal(model._last_tokens.cpu(), r_scores.max(2)[1].reshape(B))
+    # second step, fed the oracle's tokens
+    caps2 = r_scores.max(2)[1]
+    r2 = oracle.decoder(rV, rvg, caps2, r_states)
+    s2 = model.decoder(V, v_g, caps2.to(gpu_device), (h1, c1))
+    np.testing.assert_allclose(s2[0].cpu().numpy(), r2[0].numpy(), atol=LOGIT_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("case,seed,noise,fseed,B", [
+    ("ref_b4", 123, 0.0, 0, 4),
+    ("ref_b64", 123, 0.0, 0, 64),
+    ("biased_b16", 99, 0.02, 5, 16),
+])
+def test_greedy_vs_reference_golden(case, seed, noise, fseed, B, gpu_device):
+    g = load_golden(case)
+    m = _model(seed, noise)
+    feats = torch.from_numpy(synth.make_features(B, seed=fseed)).to(gpu_device)
+    ids, alpha, beta = m.sampler(feats, max_len=20)
+    ids = ids.cpu().numpy()
+    assert ids.shape == (B, 20) and ids.dtype == np.int64
+    mism = np.argwhere(ids != g["ids"])
+    assert mism.size == 0, f"token mismatch at {mism[:5].tolist()} (margins {g['margin'][tuple(mism[0])] if mism.size else None})"
+    if "alpha" in g:
+        np.testing.assert_allclose(alpha.cpu().numpy(), g["alpha"], atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(beta.cpu().numpy(), g["beta"], atol=ATT_TOL, rtol=0)
+
+
+def test_greedy_b512_vs_reference_golden(gpu_device):
+    g = load_golden("ref_b512")
+    m = _model()
+    feats = torch.from_numpy(synth.make_features(512)).to(gpu_device)
+    ids, alpha, beta = m.sampler(feats, max_len=20)
+    ids = ids.cpu().numpy()
+    mism = np.argwhere(ids != g["ids"])
+    assert mism.size == 0, f"{len(mism)} token mismatches, first at {mism[:3].tolist()}, margin there {g['margin'][tuple(mism[0])]}"
+    np.testing.assert_allclose(beta.cpu().numpy(), g["beta"], atol=ATT_TOL, rtol=0)
+
+
+def test_batch_invariance(model, gpu_device):
+    """Row i decoded inside B=300 equals row i decoded alone / inside a ragged batch, bitwise."""
+    feats = torch.from_numpy(synth.make_features(300, seed=11)).to(gpu_device)
+    ids, alpha, beta = model.sampler(feats, max_len=12)
+    for lo, hi in [(0, 1), (37, 74), (250, 300)]:
+        i2, a2, b2 = model.sampler(feats[lo:hi].contiguous(), max_len=12)
+        assert torch.equal(i2, ids[lo:hi])
+        assert torch.equal(a2, alpha[lo:hi])
+        assert torch.equal(b2, beta[lo:hi])
+
+
+def test_greedy_matches_oracle_odd_batch(model, oracle, gpu_device):
+    B = 37
+    feats = synth.make_features(B, seed=21)
+    ids, alpha, beta = model.sampler(torch.from_numpy(feats).to(gpu_device), max_len=30)  # reference default
+    r_ids, r_alpha, r_beta = oracle.sampler(torch.from_numpy(feats), max_len=30)
+    assert torch.equal(ids.cpu(), r_ids)
+    np.testing.assert_allclose(alpha.cpu().numpy(), r_alpha.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(beta.cpu().numpy(), r_beta.numpy(), atol=ATT_TOL, rtol=0)
+
+
+def test_argmax_ties_pick_first_index(gpu_device):
+    """Copy each step-0 winner's vocab row to one lower and one higher index: the logits tie
+    exactly (same weights, same accumulation order), and the lower index must win, as torch's
+    max(2)[1] returns the first maximal index (adaptive_attention.py:201)."""
+    m = _model()
+    feats = torch.from_numpy(synth.make_features(6, seed=2)).to(gpu_device)
+    ids0, _, _ = m.sampler(feats, max_len=1)
+    winners = sorted(set(ids0[:, 0].tolist()))
+    used = set(winners)
+    low, high = {}, {}
+    for tok in winners:
+        lo = next(i for i in range(tok - 1, -1, -1) if i not in used) if tok > 0 else None
+        hi = next(i for i in range(tok + 1, 10123) if i not in used)
+        used.update(x for x in (lo, hi) if x is not None)
+        low[tok], high[tok] = lo, hi
+    with torch.no_grad():
+        W = m.decoder.adaptive.mlp.weight
+        b = m.decoder.adaptive.mlp.bias
+        for tok in winners:
+            for dst in (low[tok], high[tok]):
+                if dst is not None:
+                    W[dst].copy_(W[tok])
+                    b[dst].copy_(b[tok])
+    ids1, _, _ = m.sampler(feats, max_len=1)
+    for b_, tok in enumerate(ids0[:, 0].tolist()):
+        want = low[tok] if low[tok] is not None else tok
+        assert ids1[b_, 0].item() == want
+
+
+def test_edge_shapes(model, gpu_device):
+    feats = torch.from_numpy(synth.make_features(3)).to(gpu_device)
+    ids, alpha, beta = model.sampler(feats[:0], max_len=20)
+    assert ids.shape == (0, 20) and alpha.shape == (0, 20, 49) and beta.shape == (0, 20, 1)
+    ids, alpha, beta = model.sampler(feats, max_len=0)
+    assert ids.shape == (3, 0)
+    i1, _, _ = model.sampler(feats, max_len=1)
+    i5, _, _ = model.sampler(feats, max_len=5)
+    assert torch.equal(i1, i5[:, :1])
+
+
+def test_errors_are_loud(model, gpu_device):
+    with pytest.raises(ValueError):
+        model.sampler(torch.zeros(2, 2048, 7, 6, device=gpu_device))
+    with pytest.raises(RuntimeError):
+        model.sampler(torch.zeros(2, 2048, 7, 7))
+    with pytest.raises(IndexError):
+        V, v_g, st, _, _ = model._encode(torch.from_numpy(synth.make_features(2)).to(gpu_device))
+        model.decoder(V, v_g, torch.full((2, 1), 10123, dtype=torch.int64, device=gpu_device), st)
