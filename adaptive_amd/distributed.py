@@ -1,0 +1,62 @@
+"""Multi-GPU greedy decode: one process per GPU, contiguous row shards, one all-gather of ids.
+
+Captioning is embarrassingly parallel (rows never interact: SURVEY.md §8e, and every kernel's
+per-row arithmetic is independent of the shard size), so rank r decodes rows [lo_r, hi_r) of the
+global batch with no per-step communication, then a single all-gather of the int64 token ids
+assembles [B, T] on every rank.  This replaces the reference's per-step ``nn.DataParallel``
+scatter/replicate/gather (code_src/models/baseline_attention.py:184-187,
+adaptive_attention.py:178-181).  Backend ``nccl`` is RCCL on ROCm (xGMI); ``gloo`` is used by the
+CPU tests.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous block of rows for ``rank``; the first ``total % world`` ranks get one extra row."""
+    if world < 1 or not 0 <= rank < world or total < 0:
+        raise ValueError(f"bad shard request total={total} world={world} rank={rank}")
+    q, r = divmod(total, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
+    if dist.get_backend(group) == "nccl":  # RCCL: one fused all-gather into the output buffer
+        dist.all_gather_into_tensor(out, inp, group=group)
+    else:  # gloo (CPU tests)
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
+
+
+def gather_rows(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
+    """All-gather row shards (produced with ``shard_bounds``) into the full [total, ...] tensor."""
+    world = dist.get_world_size(group)
+    counts = [shard_bounds(total, world, r)[1] - shard_bounds(total, world, r)[0] for r in range(world)]
+    rank = dist.get_rank(group)
+    if local.size(0) != counts[rank]:
+        raise ValueError(f"rank {rank} holds {local.size(0)} rows, expected {counts[rank]}")
+    width = max(counts) if counts else 0
+    if all(c == width for c in counts):
+        out = torch.empty((total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        _all_gather(out, local.contiguous(), group)
+        return out
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.size(0)] = local
+    buf = torch.empty((world * width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    _all_gather(buf, pad, group)
+    return torch.cat([buf[r * width: r * width + counts[r]] for r in range(world)], dim=0)
+
+
+def sharded_sampler(decode: Callable[[torch.Tensor, int], Tuple[torch.Tensor, ...]], images_local: torch.Tensor,
+                    total: int, max_len: int, group=None, gather_attention: bool = False):
+    """Decode this rank's rows with ``decode(images, max_len) -> (ids, alpha, beta)`` and all-gather
+    the ids (and optionally alpha/beta) to every rank."""
+    ids, alpha, beta = decode(images_local, max_len)
+    ids_all = gather_rows(ids, total, group)
+    if not gather_attention:
+        return ids_all, None, None
+    return ids_all, gather_rows(alpha, total, group), gather_rows(beta, total, group)
