@@ -225,8 +225,12 @@ class Encoder2Decoder(nn.Module):
 
     # ---- Encoder2Decoder.sampler (adaptive_attention.py:168-216) --------------------------------
     @torch.no_grad()
-    def sampler(self, images: torch.Tensor, max_len: int = 30, trace: Optional[_lib.Trace] = None):
-        """Greedy decode -> (ids [B,max_len] int64, alpha [B,max_len,49], beta [B,max_len,1])."""
+    def sampler(self, images: torch.Tensor, max_len: int = 30, trace: Optional[_lib.Trace] = None,
+                exact_vocab: bool = False):
+        """Greedy decode -> (ids [B,max_len] int64, alpha [B,max_len,49], beta [B,max_len,1]).
+
+        ``exact_vocab=True`` computes every fp32 logit; the default screens with bf16 under a rigorous
+        error bound and rescores the candidates in exact fp32 — the ids are identical."""
         images = self._check_images(images)
         model = self._model_struct()
         lib = _lib.load()
@@ -238,7 +242,7 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
                                       beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                      trace, _lib.stream_handle())
+                                      trace, _lib.DECODE_EXACT_VOCAB if exact_vocab else 0, _lib.stream_handle())
         _lib.check(rc, "greedy_decode")
         return ids, alpha, beta
 
@@ -307,6 +311,27 @@ class Encoder2Decoder(nn.Module):
         _lib.check(rc, "decode_step")
         self._last_tokens = tok_out
         return scores, alpha, beta, (h_out, c_out)
+
+    # ---- AdaptiveBlock.mlp on given rows (adaptive_attention.py:132) ----------------------------
+    @torch.no_grad()
+    def vocab_logits(self, u: torch.Tensor, cols: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Exact fp32 logits u W_m^T + b_m for u [B,H] (CUDA); all columns, or only ``cols`` [B,n]
+        (int32/int64, rescoring in the same fma order, so bit-identical to the full logits)."""
+        model = self._model_struct()
+        lib = _lib.load()
+        u = u.contiguous().float()
+        B = u.size(0)
+        with torch.cuda.device(u.device):
+            if cols is None:
+                out = torch.empty(B, self.dims.vocab, device=u.device)
+                rc = lib.aa_vocab_logits(model, B, u.data_ptr(), out.data_ptr(), _lib.stream_handle())
+            else:
+                cols = cols.to(device=u.device, dtype=torch.int32).contiguous()
+                out = torch.empty(B, cols.size(1), device=u.device)
+                rc = lib.aa_vocab_logits_at(model, B, u.data_ptr(), cols.data_ptr(), cols.size(1), out.data_ptr(),
+                                            _lib.stream_handle())
+        _lib.check(rc, "vocab_logits")
+        return out
 
     def forward(self, images, captions, lengths):
         raise NotImplementedError(

@@ -54,17 +54,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + slot;
 }
 
-// Plain row-major A loader: row `r` of the tile = global row m0 + r (zero when >= M).
+// Plain row-major A loader: row `r` of the tile = global row m0 + r.
 struct ARowMajor {
   const float* A;
   int64_t lda;
   int m0, M;
   __device__ __forceinline__ void map(int q, int& r, int& kq) const { r = q >> 3; kq = q & 7; }
+  // Rows >= M are clamped to row M-1 (a valid address) and NOT zeroed: an output row depends only
+  // on its own A row, and rows >= M are never stored.  No branch and no select between the load and
+  // its LDS store, so hipcc keeps every load of the K-step in flight under the MFMAs (an exec-masked
+  // branch or a select per load makes it wait for each load right after issuing it).
   __device__ __forceinline__ float4 load(int /*i*/, int q, int k0) const {
     const int r = q >> 3, kq = q & 7;
     const int m = m0 + r;
-    if (m >= M) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(A + (int64_t)m * lda + k0 + 4 * kq);
+    const int mc = m < M ? m : M - 1;
+    return *reinterpret_cast<const float4*>(A + (int64_t)mc * lda + k0 + 4 * kq);
   }
 };
 
@@ -145,6 +149,84 @@ __device__ __forceinline__ void gemm_mainloop(const AL& al, const WL& wl, int nk
     }
     if (more) lstore(buf ^ 1);
     __syncthreads();
+  }
+}
+
+// Same pipeline, but K-step ks accumulates into partial p = ks / (nk / NP) (NP independent chains
+// over contiguous K ranges, nk % NP == 0).  The caller combines the partials in a fixed tree; a
+// VALU re-computation of one output (8 lanes x one chain each, then the same tree) is then
+// bit-identical, which the vocab rescoring relies on.
+template <int BM, int BN, int NP, class AL, class WL>
+__device__ __forceinline__ void gemm_mainloop_np(const AL& al, const WL& wl, int nk, float* lds,
+                                                 floatx16 (&acc)[NP][BM / 64][BN / 64]) {
+  using T = Tile<BM, BN>;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[p][tm][tn][r] = 0.f;
+
+  float4 ra[T::AF4], rw[T::WF4];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < T::AF4; ++i) ra[i] = al.load(i, t + NT * i, ks * BK);
+#pragma unroll
+    for (int i = 0; i < T::WF4; ++i) rw[i] = wl.load(t + NT * i, ks * BK);
+  };
+  auto lstore = [&](int buf) {
+    float* As = lds + buf * T::STAGE;
+    float* Ws = As + BM * LDK;
+#pragma unroll
+    for (int i = 0; i < T::AF4; ++i) {
+      int r, kq;
+      al.map(t + NT * i, r, kq);
+      *reinterpret_cast<float4*>(As + r * LDK + 4 * kq) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < T::WF4; ++i) {
+      const int q = t + NT * i;
+      *reinterpret_cast<float4*>(Ws + (q >> 3) * LDK + 4 * (q & 7)) = rw[i];
+    }
+  };
+  const int per = nk / NP;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    for (int k2 = 0; k2 < per; ++k2) {
+      const int ks = p * per + k2;
+      const int buf = ks & 1;
+      const bool more = ks + 1 < nk;
+      if (more) gload(ks + 1);
+      const float* As = lds + buf * T::STAGE;
+      const float* Ws = As + BM * LDK;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        float4 a[T::TM], w[T::TN];
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm)
+          a[tm] = *reinterpret_cast<const float4*>(As + (wm * (BM / 2) + tm * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn)
+          w[tn] = *reinterpret_cast<const float4*>(Ws + (wn * (BN / 2) + tn * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < T::TN; ++tn)
+              acc[p][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a[tm], j), f4c(w[tn], j), acc[p][tm][tn], 0, 0, 0);
+      }
+      if (more) lstore(buf ^ 1);
+      __syncthreads();
+    }
   }
 }
 

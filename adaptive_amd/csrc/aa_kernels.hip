@@ -2,21 +2,26 @@
 // ("Knowing When to Look"; reference: code_src/models/adaptive_attention.py,
 // code_src/models/baseline_attention.py).  See DESIGN.md for the data layout and rooflines.
 //
-// Kernels (one launch each, all fp32):
+// Kernels (all arithmetic that defines an output is fp32):
+//   pack time (once per weight set)
+//     k_pack_lstm     W_hh / emb-part / v_g-part of W_ih and W_x re-laid in gate-interleaved tiles
+//     k_gemm_bias     table[v] = embed[v] . [W_ih(emb part); W_x(emb part)]^T   (V x 5H)
+//     k_pack_mlp      bf16 copy and row norms of W_m for the vocab screen
 //   encoder tail (once per batch)
-//     k_avgpool    a_g = AvgPool2d(7)(A)                          baseline_attention.py:46-47
-//     k_enc_v      V = relu(A^T W_a^T + b_a)   [B*49, H]           :50-51   MFMA 128x128 tiles
-//     k_enc_heads  v_g | h0 | c0 = act(a_g [W_b;W_h0;W_c0]^T + b)  :53-60   MFMA 64x64
-//     k_vwv        VWv = V W_v^T (step-invariant, hoisted)         adaptive_attention.py:34
+//     k_avgpool       a_g = AvgPool2d(7)(A)                           baseline_attention.py:46-47
+//     k_enc_v         V = relu(A^T W_a^T + b_a)  [B*49, H]             :50-51
+//     k_enc_heads     v_g | h0 | c0 = act(a_g [W_b;W_h0;W_c0]^T + b)   :53-60
+//     k_gemm_bias     VWv = V W_v^T (step-invariant, hoisted)          adaptive_attention.py:34
+//     k_gemm_bias     xg = v_g . [W_ih(v_g part); W_x(v_g part)]^T + b_ih + b_hh (step-invariant)
 //   decode step t (x T)
-//     k_lstm       x_t = [embed[tok]; v_g] gathered in the A-loader; gates GEMM over [x_t; h]
-//                  with the LSTM cell in the epilogue; sentinel pre-activation x_t W_x^T
-//                  baseline_attention.py:151-172, adaptive_attention.py:79-80
-//     k_atten      s_t, W_g h, W_s s, 49+1 tanh scores, softmax, context, beta mix, u = c_hat + h
-//                  adaptive_attention.py:26-58, 83, 132 (input of mlp)
-//     k_vocab      logits = u W_m^T + b_m with fused first-index argmax (64-bit key atomicMax)
-//                  adaptive_attention.py:132, 201
-//   k_finalize     ids [B,T] from the per-step argmax keys
+//     k_lstm          gates = table[tok] + xg + h W_hh^T; LSTM cell; sentinel s = sigm(.) tanh(c')
+//                     baseline_attention.py:151-172, adaptive_attention.py:79-83
+//     k_atten         W_g h, W_s s, 49+1 tanh scores, softmax, context, beta mix, u = c_hat + h
+//                     adaptive_attention.py:26-58, 132 (input of mlp)
+//     k_vscreen       bf16 MFMA logits with a rigorous error bound -> per-tile candidate summary
+//     k_vrescore      exact fp32 logits of the candidates (MFMA-order fma chain) + first-index argmax
+//                     adaptive_attention.py:132, 201
+//   exact-vocab path (scores output / verification): k_vocab (fp32 MFMA GEMM + fused argmax) + k_finalize
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -28,8 +33,27 @@ namespace aa {
 
 constexpr int P = 49;          // attention width == 7x7 spatial locations (adaptive_attention.py:16-19)
 constexpr int PP = 64;         // padded attention width (VWv row pitch, W_v rows)
-constexpr int MAX_H = 1024;    // k_atten keeps h and s of one row in LDS
+constexpr int MAX_H = 1024;    // k_atten keeps h and s rows in LDS
 constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Vocab-screen error bound.  For one logit, the fp32 path (k_vocab / k_vrescore) computes
+// L = fl(sum_k u_k w_k) + b and the screen computes A = fl(sum_k bf16(u_k) bf16(w_k)) + b.
+// bf16 round-to-nearest has unit roundoff 2^-8, so |bf16(u)bf16(w) - uw| <= (2^-7 + 2^-16)|uw|;
+// both fp32 accumulations add <= gamma_H * sum|uw| each (gamma_512 ~ 3.1e-5).  Hence
+// |A - L| <= (0.0078125 + 1.6e-5 + 6.2e-5 (+ bias roundings)) * sum_k |u_k w_k|
+//         <= 0.00791 * ||u||_2 ||w||_2   (Cauchy-Schwarz).
+// CEPS = 0.0085 adds ~7% slack (norms are themselves fp32 and inflated by 1e-5); EPS_REL covers
+// the bias additions.  A column n is a candidate iff A_n + eps_n >= max_m (A_m - eps_m): every
+// column holding the exact-fp32 maximum passes, every rejected column is strictly below it.
+constexpr float CEPS = 0.0085f;
+constexpr float EPS_REL = 1e-6f;
+constexpr int VS_TILE = 32;     // screen summary granule: one (lbmax, top-2 ub) per row per 32 columns
+constexpr int RS_CAP = 2048;    // candidate list capacity per row in k_vrescore (else full row)
+// Exact fp32 logits (k_vocab and the rescoring) are NP_VOCAB independent fma chains over contiguous
+// K ranges (in the MFMA k order), combined as ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)), then + bias.
+constexpr int NP_VOCAB = 8;
 
 // ---------------------------------------------------------------------------------------------
 // Packed weight layout (float offsets into aa_model.packed), 64-float aligned regions.
@@ -38,8 +62,8 @@ struct Layout {
   int E, H, V, C;
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
-  int KL, KX;    // LSTM K = 2E + H, sentinel K = 2E
-  size_t enc_a_w, enc_a_b, heads_w, heads_b, wv, wg, ws, wh, embed, lstm_w, lstm_b, sent_w, mlp_w, mlp_b;
+  int N5;        // 5H: 4 gates (packed tile order) + sentinel
+  size_t enc_a_w, enc_a_b, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn;
   size_t total_floats;
 };
 
@@ -51,7 +75,7 @@ static Layout make_layout(const aa_dims& d) {
   L.E = d.embed; L.H = d.hidden; L.V = d.vocab; L.C = d.channels;
   L.NH = L.E + 2 * L.H; L.NHp = rup(L.NH, 64);
   L.Vp = rup(L.V, 128);
-  L.KL = 2 * L.E + L.H; L.KX = 2 * L.E;
+  L.N5 = 5 * L.H;
   size_t o = 0;
   auto take = [&](size_t n) { size_t r = o; o = al64(o + n); return r; };
   L.enc_a_w = take((size_t)L.H * L.C);
@@ -62,18 +86,23 @@ static Layout make_layout(const aa_dims& d) {
   L.wg = take((size_t)P * L.H);
   L.ws = take((size_t)P * L.H);
   L.wh = take(PP);
-  L.embed = take((size_t)L.V * L.E);
-  L.lstm_w = take((size_t)4 * L.H * L.KL);
-  L.lstm_b = take((size_t)4 * L.H);
-  L.sent_w = take((size_t)L.H * L.KX);
+  L.whh = take((size_t)4 * L.H * L.H);
+  L.wemb = take((size_t)L.N5 * L.E);
+  L.wvg = take((size_t)L.N5 * L.E);
+  L.bias5 = take(L.N5);
+  L.table = take((size_t)L.V * L.N5);
   L.mlp_w = take((size_t)L.Vp * L.H);
   L.mlp_b = take(L.Vp);
+  L.mlp_wb = take((size_t)L.Vp * L.H / 2);  // bf16
+  L.mlp_wn = take(L.Vp);
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *embed, *lstm_w, *lstm_b, *sent_w, *mlp_w, *mlp_b;
+  const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
+      *mlp_b, *mlp_wn;
+  const uint16_t* mlp_wb;
 };
 
 static MP resolve(const aa_model* m, const Layout& L) {
@@ -82,8 +111,9 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.enc_a_w = b + L.enc_a_w; p.enc_a_b = b + L.enc_a_b;
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
-  p.embed = b + L.embed; p.lstm_w = b + L.lstm_w; p.lstm_b = b + L.lstm_b;
-  p.sent_w = b + L.sent_w; p.mlp_w = b + L.mlp_w; p.mlp_b = b + L.mlp_b;
+  p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
+  p.mlp_w = b + L.mlp_w; p.mlp_b = b + L.mlp_b;
+  p.mlp_wb = reinterpret_cast<const uint16_t*>(b + L.mlp_wb); p.mlp_wn = b + L.mlp_wn;
   return p;
 }
 
@@ -119,6 +149,20 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int o) {
   hi = __shfl_xor(hi, o, 64);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t x = shfl_xor_u64(k, o);
+    k = x > k ? x : k;
+  }
+  return k;
+}
+
+// fp32 -> bf16, round to nearest even (finite inputs)
+__device__ __forceinline__ uint16_t f2bf(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
 
 // ---------------------------------------------------------------------------------------------
 // E0: a_g[b, c] = (sum_p A[b, c, p]) / 49, sequential fp32 sum in p order (the order of ATen's
@@ -149,44 +193,43 @@ __global__ __launch_bounds__(256) void k_avgpool(const float* __restrict__ feats
 // ---------------------------------------------------------------------------------------------
 template <int BM>
 struct ANCHW {
-  const float* F;
-  int C, m0, M;
+  // Per-thread row base pointer computed once (the thread's row is the same for every i and
+  // K-step: q % BM == t % BM); a K-step only adds k * 49.
+  const float* base;
+  __device__ __forceinline__ void init(const float* F, int C, int m0, int M) {
+    const int m = m0 + (int)(threadIdx.x % BM);
+    const int mc = m < M ? m : M - 1;  // clamp, never zero (see ARowMajor)
+    const int b = mc / P, p = mc - b * P;
+    base = F + (int64_t)b * C * P + p;
+  }
   __device__ __forceinline__ void map(int q, int& r, int& kq) const { r = q % BM; kq = q / BM; }
   __device__ __forceinline__ float4 load(int /*i*/, int q, int k0) const {
-    const int r = q % BM, kq = q / BM;
-    const int m = m0 + r;
-    if (m >= M) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const int b = m / P, p = m - b * P;
-    const float* s = F + ((int64_t)b * C + k0 + 4 * kq) * P + p;
+    const float* s = base + (k0 + 4 * (q / BM)) * P;
     return make_float4(s[0], s[P], s[2 * P], s[3 * P]);
   }
 };
 
-__global__ __launch_bounds__(256, 2) void k_enc_v(const float* __restrict__ feats, int B, int C, int H,
-                                                  const float* __restrict__ W, const float* __restrict__ bias,
-                                                  float* __restrict__ V) {
-  constexpr int BM = 128, BN = 128;
+__global__ __launch_bounds__(256) void k_enc_v(const float* __restrict__ feats, int B, int C, int H,
+                                               const float* __restrict__ W, const float* __restrict__ bias,
+                                               float* __restrict__ V) {
+  constexpr int BM = 64, BN = 64;
   __shared__ __attribute__((aligned(16))) float lds[Tile<BM, BN>::LDS_FLOATS];
   const int M = B * P, MT = (M + BM - 1) / BM, NTn = H / BN;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int mt = L / NTn, nt = L % NTn;  // n fastest: the A tile is shared inside an XCD
-  ANCHW<BM> al{feats, C, mt * BM, M};
+  ANCHW<BM> al;
+  al.init(feats, C, mt * BM, M);
   WRowMajor wl{W, C, nt * BN};
-  floatx16 acc[2][2];
+  floatx16 acc[1][1];
   gemm_mainloop<BM, BN>(al, wl, C / BK, lds, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 1, wn = wave & 1;
+  const int col = nt * BN + wn * 32 + (lane & 31);
+  const float bv = bias[col];
 #pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < 2; ++tn) {
-      const int col = nt * BN + wn * 64 + tn * 32 + (lane & 31);
-      const float bv = bias[col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = mt * BM + wm * 64 + tm * 32 + acc_row(r, lane);
-        if (row < M) V[(int64_t)row * H + col] = reluf_(acc[tm][tn][r] + bv);
-      }
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int row = mt * BM + wm * 32 + acc_row(r, lane);
+    if (row < M) V[(int64_t)row * H + col] = reluf_(acc[0][0][r] + bv);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -220,182 +263,189 @@ __global__ __launch_bounds__(256) void k_enc_heads(const float* __restrict__ a_g
 }
 
 // ---------------------------------------------------------------------------------------------
-// E3: VWv[m, j] = V[m, :] · W_v[j, :]  (j < 64, rows >= 49 of W_v are zero).  Step-invariant:
-// the reference recomputes it every step (adaptive_attention.py:34); the values are identical.
+// Generic C[M, N] = A[M, K] · W[N, K]^T (+ bias[N]) with a row-major store (ldc), N % 64 == 0.
+// Used for VWv (encoder), xg (encoder) and the per-token table (pack time).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_vwv(const float* __restrict__ V, int M, int H, const float* __restrict__ Wv,
-                                             float* __restrict__ VWv) {
+__global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, int lda, int M, const float* __restrict__ W,
+                                                   int ldw, int N, int K, const float* __restrict__ bias,
+                                                   float* __restrict__ Cm, int64_t ldc) {
   constexpr int BM = 64, BN = 64;
   __shared__ __attribute__((aligned(16))) float lds[Tile<BM, BN>::LDS_FLOATS];
-  const int mt = blockIdx.x;
-  ARowMajor al{V, H, mt * BM, M};
-  WRowMajor wl{Wv, H, 0};
+  const int MT = (M + BM - 1) / BM, NTn = N / BN;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;
+  ARowMajor al{A, lda, mt * BM, M};
+  WRowMajor wl{W, ldw, nt * BN};
   floatx16 acc[1][1];
-  gemm_mainloop<BM, BN>(al, wl, H / BK, lds, acc);
+  gemm_mainloop<BM, BN>(al, wl, K / BK, lds, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 1, wn = wave & 1;
-  const int col = wn * 32 + (lane & 31);
+  const int col = nt * BN + wn * 32 + (lane & 31);
+  const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = mt * BM + wm * 32 + acc_row(r, lane);
-    if (row < M) VWv[(int64_t)row * PP + col] = acc[0][0][r];
+    if (row < M) Cm[(int64_t)row * ldc + col] = bias ? acc[0][0][r] + bv : acc[0][0][r];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// D1: LSTM step + sentinel pre-activation.
-//   A row b = x_t|h = [embed[tok_b] (E) ; v_g[b] (E) ; h_{t}[b] (H)], gathered by the A-loader
-//   (K-steps never straddle a segment: E % 32 == 0).
-//   N tiles 0 .. H/16-1: 64 packed columns = gates (i, f, g, o) x 16 hidden units, K = 2E + H;
-//     epilogue: c' = s(f) c + s(i) tanh(g), h' = s(o) tanh(c') (torch LSTM cell, gate order i,f,g,o).
-//   N tiles H/16 .. : 64 columns of x_t W_x^T (Sentinel.affine_x, K = 2E; the W_h h_{t-1} term
-//     multiplies zeros while sampling, adaptive_attention.py:116-122, and is skipped).
+// D1: LSTM step + sentinel.  x_t = [embed[tok]; v_g] enters through two step-invariant terms:
+//   table[tok] = embed[tok] . W_ih[:, :E]^T (pack time)   and   xg[b] = v_g[b] . W_ih[:, E:]^T + b_ih + b_hh
+// (per batch), so the step's GEMM is only h_{t-1} W_hh^T (K = H).  Columns are packed per tile of
+// 16 hidden units as (i, f, g, o) x 16; the epilogue exchanges the tile through LDS so one thread
+// sees all four gates of a unit:
+//   c' = s(f) c + s(i) tanh(g),  h' = s(o) tanh(c')            (torch LSTM cell, gate order i,f,g,o)
+//   s  = sigmoid(x W_x^T + W_h . 0) * tanh(c')                  (Sentinel, h_{t-1} = 0 while sampling,
+//                                                                adaptive_attention.py:116-122)
+// with x W_x^T = table[tok][4H + j] + xg[b][4H + j].
+// The tile then contributes its 16 units to the attention projections W_g h' and W_s s
+// (Atten.affine_g / affine_s, adaptive_attention.py:35,45): part[b][tile][j] = sum_{u in tile}
+// (j < 49 ? h'_u W_g[j][u] : s_u W_s[j-49][u]); k_atten adds the H/16 partials in tile order.
 // ---------------------------------------------------------------------------------------------
-struct AGather {
-  const float *embed, *vg, *h;
-  int E, H, m0, M;
-  int tok[2];
-  __device__ __forceinline__ void map(int q, int& r, int& kq) const { r = q >> 3; kq = q & 7; }
-  __device__ __forceinline__ float4 load(int i, int q, int k0) const {
-    const int r = q >> 3, kq = q & 7;
-    const int m = m0 + r;
-    if (m >= M) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* s;
-    if (k0 < E) s = embed + (int64_t)tok[i] * E + k0;
-    else if (k0 < 2 * E) s = vg + (int64_t)m * E + (k0 - E);
-    else s = h + (int64_t)m * H + (k0 - 2 * E);
-    return *reinterpret_cast<const float4*>(s + 4 * kq);
-  }
-};
+constexpr int PART = 128;  // partial-projection row pitch (2 x 49 used)
 
-__global__ __launch_bounds__(256) void k_lstm(int B, int E, int H, int V, const uint64_t* __restrict__ keys_prev,
-                                              const int64_t* __restrict__ tok_in, const float* __restrict__ embed,
-                                              const float* __restrict__ vg, const float* __restrict__ h_in,
-                                              const float* __restrict__ c_in, const float* __restrict__ lstm_w,
-                                              const float* __restrict__ lstm_b, const float* __restrict__ sent_w,
-                                              float* __restrict__ h_out, float* __restrict__ c_out, float* __restrict__ sx) {
+__global__ __launch_bounds__(256) void k_lstm(int B, int H, int V, const uint64_t* __restrict__ keys_prev,
+                                              const int64_t* __restrict__ tok_in, const float* __restrict__ table,
+                                              const float* __restrict__ xg, const float* __restrict__ h_in,
+                                              const float* __restrict__ c_in, const float* __restrict__ whh,
+                                              const float* __restrict__ Wg, const float* __restrict__ Ws,
+                                              float* __restrict__ h_out, float* __restrict__ c_out, float* __restrict__ s_out,
+                                              float* __restrict__ part) {
   constexpr int BM = 64, BN = 64;
   __shared__ __attribute__((aligned(16))) float lds[Tile<BM, BN>::LDS_FLOATS];
-  const int MT = (B + BM - 1) / BM, NL = H / 16, NS = H / 64, NTn = NL + NS;
+  const int MT = (B + BM - 1) / BM, NTn = H / 16;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
   const int m0 = mt * BM;
-
-  AGather al{embed, vg, h_in, E, H, m0, B, {0, 0}};
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = m0 + (t >> 3) + 32 * i;
-    int64_t tk = 1;  // <start> (adaptive_attention.py:187-190)
-    if (m < B) {
-      if (keys_prev) tk = key_token(keys_prev[m]);
-      else if (tok_in) tk = tok_in[m];
-    }
-    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
-    al.tok[i] = (int)tk;
-  }
-
+  ARowMajor al{h_in, H, m0, B};
+  WRowMajor wl{whh, H, nt * BN};
   floatx16 acc[1][1];
-  if (nt < NL) {
-    const int KL = 2 * E + H;
-    WRowMajor wl{lstm_w, KL, nt * BN};
-    gemm_mainloop<BM, BN>(al, wl, KL / BK, lds, acc);
-    // exchange the 64x64 gate tile through LDS so one thread sees all four gates of a unit
-    constexpr int CP = 68;
-    float* Cs = lds;
+  gemm_mainloop<BM, BN>(al, wl, H / BK, lds, acc);
+  constexpr int CP = 68;
+  float* Cs = lds;                 // [64][CP] gate pre-activations
+  float* Hs = lds + 64 * CP;       // [64][16] h' of the tile
+  float* Ss = Hs + 64 * 16;        // [64][16] s of the tile
+  float* Wsl = Ss + 64 * 16;       // [98][17] W_g / W_s columns of the tile's units (padded: no bank conflicts)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Cs[(wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31)] = acc[0][0][r];
-    __syncthreads();
-    const int rr = t >> 2, u0 = (t & 3) * 4, m = m0 + rr;
+  for (int r = 0; r < 16; ++r) Cs[(wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31)] = acc[0][0][r];
+  for (int i = t; i < 2 * P * 16; i += 256) {  // 98 rows x 16 units
+    const int j = i >> 4, u = i & 15;
+    const float* src = j < P ? Wg + (int64_t)j * H : Ws + (int64_t)(j - P) * H;
+    Wsl[j * 17 + u] = src[nt * 16 + u];
+  }
+  __syncthreads();
+  const int rr = t >> 2, u0 = (t & 3) * 4, m = m0 + rr;
+  {
+    const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
+    int64_t tk = 1;  // <start> (adaptive_attention.py:187-190)
+    if (keys_prev) tk = key_token(keys_prev[mc]);
+    else if (tok_in) tk = tok_in[mc];
+    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+    const int N5 = 5 * H;
+    const float* trow = table + tk * N5;
+    const float* xrow = xg + (int64_t)mc * N5;
+    const float* cr = Cs + rr * CP;
+    const int j = nt * 16 + u0;
+    float4 pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 a = *reinterpret_cast<const float4*>(trow + nt * 64 + g * 16 + u0);
+      const float4 b = *reinterpret_cast<const float4*>(xrow + nt * 64 + g * 16 + u0);
+      pre[g] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    const float4 sa = *reinterpret_cast<const float4*>(trow + 4 * H + j);
+    const float4 sb = *reinterpret_cast<const float4*>(xrow + 4 * H + j);
+    const float4 cprev = *reinterpret_cast<const float4*>(c_in + (int64_t)mc * H + j);
+    float hn[4], cn[4], sn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float gi = cr[0 + u0 + q] + f4c(pre[0], q);
+      const float gf = cr[16 + u0 + q] + f4c(pre[1], q);
+      const float gg = cr[32 + u0 + q] + f4c(pre[2], q);
+      const float go = cr[48 + u0 + q] + f4c(pre[3], q);
+      const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+      cn[q] = f_ * f4c(cprev, q) + i_ * g_;
+      const float tc = tanhf(cn[q]);
+      hn[q] = o_ * tc;
+      sn[q] = sigmoidf_(f4c(sa, q) + f4c(sb, q)) * tc;
+    }
+    *reinterpret_cast<float4*>(Hs + rr * 16 + u0) = make_float4(hn[0], hn[1], hn[2], hn[3]);
+    *reinterpret_cast<float4*>(Ss + rr * 16 + u0) = make_float4(sn[0], sn[1], sn[2], sn[3]);
     if (m < B) {
-      const float* cr = Cs + rr * CP;
-      const float* bb = lstm_b + nt * 64;
-      const int j = nt * 16 + u0;
-      const float4 cprev = *reinterpret_cast<const float4*>(c_in + (int64_t)m * H + j);
-      float hn[4], cn[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float gi = cr[0 + u0 + q] + bb[0 + u0 + q];
-        const float gf = cr[16 + u0 + q] + bb[16 + u0 + q];
-        const float gg = cr[32 + u0 + q] + bb[32 + u0 + q];
-        const float go = cr[48 + u0 + q] + bb[48 + u0 + q];
-        const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
-        const float c = f4c(cprev, q);
-        cn[q] = f_ * c + i_ * g_;
-        hn[q] = o_ * tanhf(cn[q]);
-      }
       *reinterpret_cast<float4*>(c_out + (int64_t)m * H + j) = make_float4(cn[0], cn[1], cn[2], cn[3]);
       *reinterpret_cast<float4*>(h_out + (int64_t)m * H + j) = make_float4(hn[0], hn[1], hn[2], hn[3]);
+      *reinterpret_cast<float4*>(s_out + (int64_t)m * H + j) = make_float4(sn[0], sn[1], sn[2], sn[3]);
     }
-  } else {
-    const int st = nt - NL, KX = 2 * E;
-    WRowMajor wl{sent_w, KX, st * BN};
-    gemm_mainloop<BM, BN>(al, wl, KX / BK, lds, acc);
-    const int col = st * BN + wn * 32 + (lane & 31);
+  }
+  __syncthreads();
+  // partial projections: thread -> j = t % 128 (valid < 98), rows t/128, t/128 + 2, ...
+  const int jp = t & 127;
+  if (jp < 2 * P) {
+    float w[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wm * 32 + acc_row(r, lane);
-      if (row < B) sx[(int64_t)row * H + col] = acc[0][0][r];
+    for (int u = 0; u < 16; ++u) w[u] = Wsl[jp * 17 + u];
+    const float* vals = jp < P ? Hs : Ss;
+    for (int r = t >> 7; r < BM; r += 2) {
+      const int mr = m0 + r;
+      if (mr >= B) break;
+      float a = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a = __builtin_fmaf(vals[r * 16 + u], w[u], a);
+      part[((int64_t)mr * NTn + nt) * PART + jp] = a;
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// D2: adaptive attention for one row per workgroup (Atten.forward, adaptive_attention.py:26-58).
-//   s     = sigmoid(x W_x^T) * tanh(c_t)                               (:79-83)
-//   hg    = W_g h_t,  ss = W_s s_t                                     (:35, :45)
+// D2: adaptive attention, one row per workgroup (Atten.forward, adaptive_attention.py:26-58).
+//   hg    = W_g h_t,  ss = W_s s_t  (sum of the LSTM tiles' partials)   (:35, :45)
 //   z_k   = w_h . tanh(VWv[k] + hg),  k < 49;  z_s = w_h . tanh(ss + hg)  (:38, :47)
 //   alpha = softmax_49(z); beta = softmax_50([z; z_s])[49]              (:39, :51-55)
 //   c_t   = sum_k alpha_k V[k];  u = beta s + (1 - beta) c_t + h_t       (:42, :56, :132)
+// Also emits bf16(u) and ||u||_2 for the vocab screen.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_atten(int B, int H, const float* __restrict__ h_new, const float* __restrict__ c_new,
-                                               const float* __restrict__ sx, const float* __restrict__ Vf,
-                                               const float* __restrict__ VWv, const float* __restrict__ Wg,
-                                               const float* __restrict__ Ws, const float* __restrict__ wh,
-                                               float* __restrict__ alpha_out, int64_t alpha_ld,
-                                               float* __restrict__ beta_out, int64_t beta_ld, float* __restrict__ u_out) {
-  __shared__ __attribute__((aligned(16))) float sh_h[MAX_H];
-  __shared__ __attribute__((aligned(16))) float sh_s[MAX_H];
-  __shared__ float proj[2 * PP];
+__global__ __launch_bounds__(256) void k_atten(int B, int H, int NTL, const float* __restrict__ h_new,
+                                               const float* __restrict__ s_new, const float* __restrict__ part,
+                                               const float* __restrict__ Vf, const float* __restrict__ VWv,
+                                               const float* __restrict__ wh, float* __restrict__ alpha_out,
+                                               int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
+                                               float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
+                                               float* __restrict__ unorm) {
+  __shared__ float proj[PART];
   __shared__ float zs[PP];
   __shared__ float sh_alpha[PP];
   __shared__ float sh_beta;
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const float* hb = h_new + (int64_t)b * H;
-  const float* cb = c_new + (int64_t)b * H;
-  const float* xb = sx + (int64_t)b * H;
-  for (int d = t; d < H; d += 256) {
-    sh_h[d] = hb[d];
-    sh_s[d] = sigmoidf_(xb[d]) * tanhf(cb[d]);
+  __shared__ float sh_norm[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = blockIdx.x;
+  // 1) projections: fixed tile order
+  if (t < 2 * P) {
+    const float* pp = part + (int64_t)b * NTL * PART + t;
+    float a = 0.f;
+    for (int i = 0; i < NTL; ++i) a += pp[(int64_t)i * PART];
+    proj[t] = a;
   }
   __syncthreads();
-  // 98 dot products of length H: wave w takes j = w, w+4, ...; lanes cover H in float4s.
-  for (int j = w; j < 2 * P; j += 4) {
-    const float* wrow = j < P ? Wg + (int64_t)j * H : Ws + (int64_t)(j - P) * H;
-    const float* vec = j < P ? sh_h : sh_s;
-    float acc = 0.f;
-    for (int d = lane * 4; d < H; d += 256) {
-      const float4 a = *reinterpret_cast<const float4*>(wrow + d);
-      const float4 v = *reinterpret_cast<const float4*>(vec + d);
-      acc += a.x * v.x + a.y * v.y + a.z * v.z + a.w * v.w;
+  // 2) scores: item k (0..49) by a quad of lanes, j strided by 4, quad combined in fixed order
+  {
+    const int k = t >> 2, q = t & 3;
+    float z = 0.f;
+    if (k <= P) {
+      const float* vw = VWv + ((int64_t)b * P + k) * PP;
+      for (int j = q; j < P; j += 4) {
+        const float x = (k < P ? vw[j] : proj[P + j]) + proj[j];
+        z = __builtin_fmaf(wh[j], tanhf(x), z);
+      }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) proj[j] = acc;
+    const float z1 = __shfl_xor(z, 1, 64);
+    const float z2 = __shfl_xor(z, 2, 64);
+    const float z3 = __shfl_xor(z, 3, 64);
+    // lane q0 of the quad holds s0; (s0 + s1) + (s2 + s3) in a fixed association
+    if (q == 0 && k <= P) zs[k] = (z + z1) + (z2 + z3);
   }
   __syncthreads();
-  // z_k (k < 49) and z_s (k == 49): lanes over j < 49
-  const float* vwv = VWv + (int64_t)b * P * PP;
-  const float whj = lane < P ? wh[lane] : 0.f;
-  const float hgj = lane < P ? proj[lane] : 0.f;
-  for (int k = w; k <= P; k += 4) {
-    float term = 0.f;
-    if (lane < P) {
-      const float x = (k < P ? vwv[k * PP + lane] : proj[P + lane]) + hgj;
-      term = whj * tanhf(x);
-    }
-    term = wave_sum(term);
-    if (lane == 0) zs[k] = term;
-  }
-  __syncthreads();
+  // 3) softmax (wave 0)
   if (w == 0) {
     const float z = lane < P ? zs[lane] : -INFINITY;
     const float zsn = zs[P];
@@ -418,59 +468,314 @@ __global__ __launch_bounds__(256) void k_atten(int B, int H, const float* __rest
     }
   }
   __syncthreads();
+  // 4) context + u
   const float beta = sh_beta;
   const float* vb = Vf + (int64_t)b * P * H;
+  float nsq = 0.f;
   for (int d = t; d < H; d += 256) {
     float c = 0.f;
 #pragma unroll 7
-    for (int k = 0; k < P; ++k) c += sh_alpha[k] * vb[(int64_t)k * H + d];
-    const float chat = beta * sh_s[d] + (1.f - beta) * c;
-    u_out[(int64_t)b * H + d] = chat + sh_h[d];
+    for (int k = 0; k < P; ++k) c = __builtin_fmaf(sh_alpha[k], vb[(int64_t)k * H + d], c);
+    const float chat = __builtin_fmaf(beta, s_new[(int64_t)b * H + d], (1.f - beta) * c);
+    const float u = chat + h_new[(int64_t)b * H + d];
+    nsq = __builtin_fmaf(u, u, nsq);
+    u_out[(int64_t)b * H + d] = u;
+    if (ub_out) ub_out[(int64_t)b * H + d] = f2bf(u);
+  }
+  if (unorm) {
+    nsq = wave_sum(nsq);
+    if (lane == 0) sh_norm[w] = nsq;
+    __syncthreads();
+    if (t == 0) unorm[b] = sqrtf((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) * 1.00001f;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// D3: logits = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132) with the argmax of
-// sampler (:201) fused into the epilogue: per-row max over the tile's columns by 64-bit keys
-// (lane shuffles, then LDS across the two column waves), one atomicMax per row per workgroup.
+// D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a 64x64
+// tile (4 waves 2x2, v_mfma_f32_32x32x16_bf16, operands straight from L2), then per (row, tile):
+//   lbmax = max_n (A_n - eps_n),  (ub1, idx1) = top of A_n + eps_n,  ub2 = second largest upper bound
+// with eps_n = CEPS ||u|| ||w_n|| + EPS_REL |A_n| (see CEPS).  Summary -> summ[row][tile] (16 B).
+// ---------------------------------------------------------------------------------------------
+struct Top2 {
+  float lb, ub1, ub2;
+  int idx;
+};
+__device__ __forceinline__ Top2 top2_merge(Top2 a, Top2 b) {
+  Top2 r;
+  r.lb = fmaxf(a.lb, b.lb);
+  if (a.ub1 > b.ub1 || (a.ub1 == b.ub1 && a.idx <= b.idx)) {
+    r.ub1 = a.ub1; r.idx = a.idx; r.ub2 = fmaxf(a.ub2, b.ub1);
+  } else {
+    r.ub1 = b.ub1; r.idx = b.idx; r.ub2 = fmaxf(b.ub2, a.ub1);
+  }
+  return r;
+}
+__device__ __forceinline__ Top2 shfl_xor_top2(Top2 a, int o) {
+  Top2 r;
+  r.lb = __shfl_xor(a.lb, o, 64);
+  r.ub1 = __shfl_xor(a.ub1, o, 64);
+  r.ub2 = __shfl_xor(a.ub2, o, 64);
+  r.idx = __shfl_xor(a.idx, o, 64);
+  return r;
+}
+
+// Screen tile: 128 rows x 128 columns per workgroup, K in 64-wide bf16 steps staged through
+// double-buffered LDS (global->register prefetch of step k+1 under the MFMAs of step k); each
+// wave owns 64 x 64 = 2 x 2 blocks of v_mfma_f32_32x32x16_bf16.
+constexpr int SC_BM = 128, SC_BN = 128, SC_BK = 64, SC_LD = SC_BK + 8;  // LDS row pitch in bf16
+__global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp, const uint16_t* __restrict__ ub,
+                                                    const float* __restrict__ unorm, const uint16_t* __restrict__ wb,
+                                                    const float* __restrict__ wn, const float* __restrict__ bias,
+                                                    float4* __restrict__ summ) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (SC_BM + SC_BN) * SC_LD];
+  __shared__ float un_s[SC_BM];
+  const int NTn = Vp / VS_TILE, NTs = Vp / SC_BN, MT = (B + SC_BM - 1) / SC_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTs);
+  const int nt = L / MT, mt = L % MT;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn_ = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int m0 = mt * SC_BM, n0 = nt * SC_BN;
+  if (t < SC_BM) un_s[t] = unorm[m0 + t < B ? m0 + t : B - 1];
+  // staging map: 16-B chunk q = t + 256 i (i < 4) -> row (t >> 3) + 32 i, chunk t & 7 (8 bf16)
+  const int sr = t >> 3, sc = t & 7;
+  int64_t aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + sr + 32 * i;
+    aoff[i] = (int64_t)(m < B ? m : B - 1) * H + 8 * sc;  // clamp, never zero (rows >= B are not stored)
+  }
+  const uint16_t* wbase = wb + (int64_t)(n0 + sr) * H + 8 * sc;
+  u32x4 ra[4], rw[4];
+#define SC_GLOAD(ks)                                                                                  \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                     \
+    ra[i] = *reinterpret_cast<const u32x4*>(ub + aoff[i] + (ks) * SC_BK);                              \
+    rw[i] = *reinterpret_cast<const u32x4*>(wbase + (int64_t)32 * i * H + (ks) * SC_BK);               \
+  }
+#define SC_LSTORE(buf)                                                                                \
+  {                                                                                                   \
+    uint16_t* As_ = lds + (buf) * (SC_BM + SC_BN) * SC_LD;                                            \
+    uint16_t* Ws_ = As_ + SC_BM * SC_LD;                                                              \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                   \
+      *reinterpret_cast<u32x4*>(As_ + (sr + 32 * i) * SC_LD + 8 * sc) = ra[i];                          \
+      *reinterpret_cast<u32x4*>(Ws_ + (sr + 32 * i) * SC_LD + 8 * sc) = rw[i];                          \
+    }                                                                                                 \
+  }
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  const int nk = H / SC_BK;
+  SC_GLOAD(0)
+  SC_LSTORE(0)
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) { SC_GLOAD(ks + 1) }
+    const uint16_t* As = lds + buf * (SC_BM + SC_BN) * SC_LD;
+    const uint16_t* Ws = As + SC_BM * SC_LD;
+#pragma unroll
+    for (int kk = 0; kk < SC_BK / 16; ++kk) {
+      bf16x8 fa[2], fw[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        fa[a] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + a * 32 + li) * SC_LD + 16 * kk + 8 * lh);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        fw[c] = *reinterpret_cast<const bf16x8*>(Ws + (wn_ * 64 + c * 32 + li) * SC_LD + 16 * kk + 8 * lh);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fw[c], acc[a][c], 0, 0, 0);
+    }
+    if (more) SC_LSTORE(buf ^ 1)
+    __syncthreads();
+  }
+#undef SC_GLOAD
+#undef SC_LSTORE
+  // epilogue: per wave, each 32-row block's (lb, ub) -> a private LDS slab; 2 lanes per row each
+  // summarise one 32-column granule (lbmax, top-2 ub) -> summ[row][col / 32].
+  float2* slab = reinterpret_cast<float2*>(lds) + wave * 32 * 65;  // [32][65] per wave
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = n0 + wn_ * 64 + c * 32 + li;
+      const bool valid = col < V;
+      const float bv = bias[col], wnv = wn[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = acc_row(r, lane);
+        const float x = acc[a][c][r] + bv;
+        const float eps = CEPS * un_s[wm * 64 + a * 32 + rl] * wnv + EPS_REL * fabsf(x);
+        slab[rl * 65 + c * 32 + li] = valid ? make_float2(x - eps, x + eps) : make_float2(-INFINITY, -INFINITY);
+      }
+    }
+    __syncthreads();
+    {
+      const int rl = lane >> 1, hq = lane & 1;
+      Top2 x{-INFINITY, -INFINITY, -INFINITY, 0};
+      const int cbase = n0 + wn_ * 64 + hq * 32;
+      for (int cc = 0; cc < 32; ++cc) {
+        const float2 v = slab[rl * 65 + hq * 32 + cc];
+        x.lb = fmaxf(x.lb, v.x);
+        if (v.y > x.ub1) { x.ub2 = x.ub1; x.ub1 = v.y; x.idx = cbase + cc; }
+        else x.ub2 = fmaxf(x.ub2, v.y);
+      }
+      const int row = m0 + wm * 64 + a * 32 + rl;
+      if (row < B) summ[(int64_t)row * NTn + cbase / VS_TILE] = make_float4(x.lb, x.ub1, x.ub2, __int_as_float(x.idx));
+    }
+    __syncthreads();
+  }
+}
+
+// Exact fp32 logit of one column, computed by a group of 8 lanes (lane8 = 0..7): lane8 j runs the
+// fma chain of partial j (K-steps [j*per, (j+1)*per) of 32, in the MFMA k order: pairs (s, 16+s)),
+// then the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) over xor-1/2/4 shuffles, then + bias.
+// Bit-identical to k_vocab (gemm_mainloop_np<.., NP_VOCAB>).  All 8 lanes return the logit.
+// u is read from LDS (urow), w straight from memory (each lane 4*32*per contiguous bytes).
+__device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, const float* __restrict__ wrow, int H,
+                                              float b, int lane8) {
+  const int per = H / (32 * NP_VOCAB);
+  const int k0 = lane8 * per * 32;
+  float acc = 0.f;
+  for (int ks = 0; ks < per; ++ks) {
+    float4 w[8], u[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      w[q] = *reinterpret_cast<const float4*>(wrow + k0 + 32 * ks + 4 * q);
+      u[q] = *reinterpret_cast<const float4*>(urow + k0 + 32 * ks + 4 * q);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      acc = __builtin_fmaf(f4c(u[s >> 2], s & 3), f4c(w[s >> 2], s & 3), acc);
+      acc = __builtin_fmaf(f4c(u[4 + (s >> 2)], s & 3), f4c(w[4 + (s >> 2)], s & 3), acc);
+    }
+  }
+  acc = acc + __shfl_xor(acc, 1, 64);
+  acc = acc + __shfl_xor(acc, 2, 64);
+  acc = acc + __shfl_xor(acc, 4, 64);
+  return acc + b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// D3b (greedy path): one workgroup (4 waves) per row.  M = max over granules of lbmax; candidates
+// = idx1 of granules with ub1 >= M, plus every column of granules with ub2 >= M (two candidates in
+// one granule).  32 candidates are scored per pass (8 lanes each, exact_logit8); first-index argmax
+// -> keys[row], ids[row, t].  A list longer than RS_CAP falls back to every column (correct, slow).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, const float* __restrict__ u,
+                                                  const float4* __restrict__ summ, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, uint64_t* __restrict__ keys,
+                                                  int64_t* __restrict__ ids, int T, int t_step) {
+  __shared__ __attribute__((aligned(16))) float urow[MAX_H];
+  __shared__ int cand[RS_CAP];
+  __shared__ int ncand;
+  __shared__ float wmax[4];
+  __shared__ uint64_t wbest[4];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int NTn = Vp / VS_TILE;
+  for (int d = 4 * t; d < H; d += 1024) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
+  if (t == 0) ncand = 0;
+  const float4* sm = summ + (int64_t)b * NTn;
+  float mlb = -INFINITY;
+  for (int i = t; i < NTn; i += 256) mlb = fmaxf(mlb, sm[i].x);
+  mlb = wave_max(mlb);
+  if (lane == 0) wmax[w] = mlb;
+  __syncthreads();
+  mlb = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  for (int i = t; i < NTn; i += 256) {
+    const float4 s = sm[i];
+    if (s.z >= mlb) {  // >= 2 candidates in this granule: take all of its columns
+      const int pos = atomicAdd(&ncand, VS_TILE);
+      for (int c = 0; c < VS_TILE; ++c)
+        if (pos + c < RS_CAP) cand[pos + c] = i * VS_TILE + c;
+    } else if (s.y >= mlb) {
+      const int pos = atomicAdd(&ncand, 1);
+      if (pos < RS_CAP) cand[pos] = __float_as_int(s.w);
+    }
+  }
+  __syncthreads();
+  const bool all = ncand > RS_CAP;
+  const int n = all ? V : ncand;
+  const int g = t >> 3, lane8 = t & 7;
+  uint64_t best = 0;
+  for (int i = g; i < n; i += 32) {
+    int col = all ? i : cand[i];
+    const bool ok = col < V;
+    col = ok ? col : V - 1;
+    const float x = exact_logit8(urow, W + (int64_t)col * H, H, bias[col], lane8);
+    if (ok) {
+      const uint64_t k = argmax_key(x, col);
+      best = k > best ? k : best;
+    }
+  }
+  best = wave_max_u64(best);
+  if (lane == 0) wbest[w] = best;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t k = wbest[0];
+    for (int i = 1; i < 4; ++i) k = wbest[i] > k ? wbest[i] : k;
+    keys[b] = k;
+    if (ids) ids[(int64_t)b * T + t_step] = key_token(k);
+  }
+}
+
+// Exact fp32 logits of selected columns (cols [B][n], -1 = skip) -> out [B][n]; same arithmetic.
+__global__ __launch_bounds__(256) void k_logits_at(int H, int V, const float* __restrict__ u, const int32_t* __restrict__ cols,
+                                                   int n, const float* __restrict__ W, const float* __restrict__ bias,
+                                                   float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float urow[MAX_H];
+  const int b = blockIdx.x, t = threadIdx.x;
+  for (int d = 4 * t; d < H; d += 1024) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
+  __syncthreads();
+  const int g = t >> 3, lane8 = t & 7;
+  for (int i = g; i < n; i += 32) {
+    const int c = cols[(int64_t)b * n + i];
+    const bool ok = c >= 0 && c < V;
+    const int col = ok ? c : 0;
+    const float x = exact_logit8(urow, W + (int64_t)col * H, H, bias[col], lane8);
+    if (lane8 == 0) out[(int64_t)b * n + i] = ok ? x : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// D3 (exact path): logits = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132) with the
+// argmax of sampler (:201) fused into the epilogue: per-row max over the tile's columns by 64-bit
+// keys (lane shuffles, then LDS across the two column waves), one atomicMax per row per workgroup.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, const float* __restrict__ u,
                                                const float* __restrict__ W, const float* __restrict__ bias,
                                                float* __restrict__ scores, uint64_t* __restrict__ keys) {
-  constexpr int BM = 64, BN = 128;
+  constexpr int BM = 64, BN = 64;
   __shared__ __attribute__((aligned(16))) float lds[Tile<BM, BN>::LDS_FLOATS];
   const int MT = (B + BM - 1) / BM, NTn = Vp / BN;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;
   ARowMajor al{u, H, mt * BM, B};
   WRowMajor wl{W, H, nt * BN};
-  floatx16 acc[1][2];
-  gemm_mainloop<BM, BN>(al, wl, H / BK, lds, acc);
+  floatx16 acc[NP_VOCAB][1][1];
+  gemm_mainloop_np<BM, BN, NP_VOCAB>(al, wl, H / BK, lds, acc);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int col = nt * BN + wn * 32 + (lane & 31);
+  const bool valid = col < V;
+  const float bv = bias[col];
   uint64_t best[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) best[r] = 0;
-#pragma unroll
-  for (int tn = 0; tn < 2; ++tn) {
-    const int col = nt * BN + wn * 64 + tn * 32 + (lane & 31);
-    const bool valid = col < V;
-    const float bv = bias[col];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float x = acc[0][tn][r] + bv;
-      const int row = mt * BM + wm * 32 + acc_row(r, lane);
-      if (scores && valid && row < B) scores[(int64_t)row * V + col] = x;
-      const uint64_t k = valid ? argmax_key(x, col) : 0ull;
-      best[r] = k > best[r] ? k : best[r];
-    }
-  }
-#pragma unroll
   for (int r = 0; r < 16; ++r) {
-    uint64_t k = best[r];
+    const float p01 = acc[0][0][0][r] + acc[1][0][0][r], p23 = acc[2][0][0][r] + acc[3][0][0][r];
+    const float p45 = acc[4][0][0][r] + acc[5][0][0][r], p67 = acc[6][0][0][r] + acc[7][0][0][r];
+    const float x = ((p01 + p23) + (p45 + p67)) + bv;
+    const int row = mt * BM + wm * 32 + acc_row(r, lane);
+    if (scores && valid && row < B) scores[(int64_t)row * V + col] = x;
+    uint64_t k = valid ? argmax_key(x, col) : 0ull;
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
-      const uint64_t x = shfl_xor_u64(k, o);
-      k = x > k ? x : k;
+      const uint64_t y = shfl_xor_u64(k, o);
+      k = y > k ? y : k;
     }
     best[r] = k;
   }
@@ -483,7 +788,7 @@ __global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, cons
   if (t < 64) {
     const uint64_t a = red[t], c = red[64 + t];
     const int row = mt * BM + t;
-    if (row < B) atomicMax(reinterpret_cast<unsigned long long*>(keys + row), (unsigned long long)(a > c ? a : c));
+    if (row < B && keys) atomicMax(reinterpret_cast<unsigned long long*>(keys + row), (unsigned long long)(a > c ? a : c));
   }
 }
 
@@ -497,24 +802,44 @@ __global__ void k_finalize(const uint64_t* __restrict__ keys, int B, int T, int6
 // ---------------------------------------------------------------------------------------------
 // packing / synthetic data
 // ---------------------------------------------------------------------------------------------
-// dst row r (r < dst_rows) = src row r for r < rows, zeros otherwise; cols contiguous.
-__global__ void k_copy_rows(const float* __restrict__ src, int rows, int cols, float* __restrict__ dst, int dst_rows) {
-  const int r = blockIdx.x;
-  if (r >= dst_rows) return;
-  for (int c = threadIdx.x; c < cols; c += blockDim.x)
-    dst[(int64_t)r * cols + c] = (src && r < rows) ? src[(int64_t)r * cols + c] : 0.f;
+// Gate-interleaved LSTM tiles: packed row r = tile*64 + gate*16 + unit  <-  reference row
+// gate*H + tile*16 + unit of W_ih / W_hh / biases (gate order i, f, g, o); rows 4H + j of the
+// emb / v_g parts are W_x row j (sentinel).
+__global__ void k_pack_lstm(const float* __restrict__ w_ih, const float* __restrict__ w_hh, const float* __restrict__ b_ih,
+                            const float* __restrict__ b_hh, const float* __restrict__ w_x, int E, int H,
+                            float* __restrict__ whh, float* __restrict__ wemb, float* __restrict__ wvg, float* __restrict__ bias5) {
+  const int r = blockIdx.x;  // 0 .. 5H-1
+  const int KX = 2 * E;
+  if (r < 4 * H) {
+    const int tile = r / 64, g = (r % 64) / 16, un = r % 16;
+    const int src = g * H + tile * 16 + un;
+    for (int k = threadIdx.x; k < E; k += blockDim.x) {
+      wemb[(int64_t)r * E + k] = w_ih[(int64_t)src * KX + k];
+      wvg[(int64_t)r * E + k] = w_ih[(int64_t)src * KX + E + k];
+    }
+    for (int k = threadIdx.x; k < H; k += blockDim.x) whh[(int64_t)r * H + k] = w_hh[(int64_t)src * H + k];
+    if (threadIdx.x == 0) bias5[r] = b_ih[src] + b_hh[src];
+  } else {
+    const int j = r - 4 * H;
+    for (int k = threadIdx.x; k < E; k += blockDim.x) {
+      wemb[(int64_t)r * E + k] = w_x[(int64_t)j * KX + k];
+      wvg[(int64_t)r * E + k] = w_x[(int64_t)j * KX + E + k];
+    }
+    if (threadIdx.x == 0) bias5[r] = 0.f;
+  }
 }
 
-// LSTM weights: packed row r = tile*64 + gate*16 + unit  <-  [W_ih | W_hh] row gate*H + tile*16 + unit
-__global__ void k_pack_lstm(const float* __restrict__ w_ih, const float* __restrict__ w_hh, const float* __restrict__ b_ih,
-                            const float* __restrict__ b_hh, int E, int H, float* __restrict__ w, float* __restrict__ bsum) {
-  const int r = blockIdx.x;
-  const int tile = r / 64, g = (r % 64) / 16, un = r % 16;
-  const int src = g * H + tile * 16 + un;
-  const int KX = 2 * E, KL = KX + H;
-  for (int k = threadIdx.x; k < KX; k += blockDim.x) w[(int64_t)r * KL + k] = w_ih[(int64_t)src * KX + k];
-  for (int k = threadIdx.x; k < H; k += blockDim.x) w[(int64_t)r * KL + KX + k] = w_hh[(int64_t)src * H + k];
-  if (threadIdx.x == 0) bsum[r] = b_ih[src] + b_hh[src];
+// bf16 copy of W_m (zero rows beyond V) and inflated row norms ||w_n||_2 for the screen bound.
+__global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, uint16_t* __restrict__ wb, float* __restrict__ wn) {
+  const int n = blockIdx.x, lane = threadIdx.x;  // 64 threads
+  float s = 0.f;
+  for (int k = lane; k < H; k += 64) {
+    const float x = n < V ? w[(int64_t)n * H + k] : 0.f;
+    wb[(int64_t)n * H + k] = f2bf(x);
+    s += x * x;
+  }
+  s = wave_sum(s);
+  if (lane == 0) wn[n] = sqrtf(s) * 1.00001f;
 }
 
 __device__ __forceinline__ uint64_t splitmix(uint64_t z) {
@@ -534,7 +859,7 @@ __global__ void k_synth_uniform(float* __restrict__ dst, int64_t n, uint64_t key
 }  // namespace aa
 
 // =============================================================================================
-// C-ABI
+// C-ABI  (exported functions get C linkage and default visibility from adaptive_amd.h)
 // =============================================================================================
 using namespace aa;
 
@@ -551,7 +876,11 @@ static int launch_status() {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// (exported functions get C linkage and default visibility from their declarations in adaptive_amd.h)
+static void gemm_bias(const float* A, int lda, int M, const float* W, int ldw, int N, int K, const float* bias, float* C,
+                      int64_t ldc, hipStream_t s) {
+  const int MT = (M + 63) / 64, NTn = N / 64;
+  hipLaunchKernelGGL(k_gemm_bias, dim3(MT * NTn), dim3(256), 0, s, A, lda, M, W, ldw, N, K, bias, C, ldc);
+}
 
 int aa_abi_version(void) { return AA_ABI_VERSION; }
 
@@ -559,7 +888,7 @@ const char* aa_error_string(int code) {
   switch (code) {
     case AA_OK: return "ok";
     case AA_ERR_NULL: return "a required pointer is NULL";
-    case AA_ERR_DIMS: return "unsupported model dimensions (need embed%32==0, hidden%128==0, hidden<=1024, vocab>=1, channels%32==0, spatial==49)";
+    case AA_ERR_DIMS: return "unsupported model dimensions (need embed%32==0, hidden%256==0, hidden<=1024, vocab>=1, channels%32==0, spatial==49)";
     case AA_ERR_SHAPE: return "bad batch size or step count";
     case AA_ERR_BUFFER: return "packed-weight or workspace buffer too small";
     case AA_ERR_ALIGN: return "a device pointer is not 16-byte aligned";
@@ -569,7 +898,7 @@ const char* aa_error_string(int code) {
 
 int aa_check_dims(const aa_dims* d) {
   if (!d) return AA_ERR_NULL;
-  if (d->embed <= 0 || d->embed % 32 || d->hidden <= 0 || d->hidden % 128 || d->hidden > MAX_H || d->vocab < 1 ||
+  if (d->embed <= 0 || d->embed % 32 || d->hidden <= 0 || d->hidden % 256 || d->hidden > MAX_H || d->vocab < 1 ||
       d->channels <= 0 || d->channels % 32 || d->spatial != P)
     return AA_ERR_DIMS;
   return AA_OK;
@@ -602,6 +931,7 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                         w->att_affine_h_w, w->mlp_w, w->mlp_b};
   for (const float* p : req)
     if (!p) return AA_ERR_NULL;
+  if (!al16(w->embed_w)) return AA_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   float* base = static_cast<float*>(m->packed);
   const int E = L.E, H = L.H, V = L.V, C = L.C;
@@ -621,22 +951,24 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   AA_TRY(cp(w->att_affine_g_w, L.wg, (size_t)P * H));
   AA_TRY(cp(w->att_affine_s_w, L.ws, (size_t)P * H));
   AA_TRY(cp(w->att_affine_h_w, L.wh, P));
-  AA_TRY(cp(w->embed_w, L.embed, (size_t)V * E));
-  AA_TRY(cp(w->sent_affine_x_w, L.sent_w, (size_t)H * 2 * E));
   AA_TRY(cp(w->mlp_w, L.mlp_w, (size_t)V * H));        // rows V..Vp-1 stay zero
   AA_TRY(cp(w->mlp_b, L.mlp_b, V));
-  hipLaunchKernelGGL(k_pack_lstm, dim3(4 * H), dim3(256), 0, s, w->lstm_w_ih, w->lstm_w_hh, w->lstm_b_ih,
-                     w->lstm_b_hh, E, H, base + L.lstm_w, base + L.lstm_b);
+  hipLaunchKernelGGL(k_pack_lstm, dim3(L.N5), dim3(256), 0, s, w->lstm_w_ih, w->lstm_w_hh, w->lstm_b_ih, w->lstm_b_hh,
+                     w->sent_affine_x_w, E, H, base + L.whh, base + L.wemb, base + L.wvg, base + L.bias5);
+  // table[v] = embed[v] . [W_ih(emb part) (packed gate order); W_x(emb part)]^T
+  gemm_bias(w->embed_w, E, V, base + L.wemb, E, L.N5, E, nullptr, base + L.table, L.N5, s);
+  hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H,
+                     reinterpret_cast<uint16_t*>(base + L.mlp_wb), base + L.mlp_wn);
   return launch_status();
 }
 
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
-                          float* h0, float* c0, float* VWv, hipStream_t s) {
+                          float* h0, float* c0, float* VWv, float* xg, hipStream_t s) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
   hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, feats, nch, a_g);
   {
-    const int M = B * P, MT = (M + 127) / 128, NTn = H / 128;
+    const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
   }
   {
@@ -644,10 +976,8 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, s, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
                        v_g, h0, c0);
   }
-  if (VWv) {
-    const int M = B * P;
-    hipLaunchKernelGGL(k_vwv, dim3((M + 63) / 64), dim3(256), 0, s, V, M, H, p.wv, VWv);
-  }
+  if (VWv) gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
+  if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, s);
   return launch_status();
 }
 
@@ -659,8 +989,8 @@ int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g
   if (B < 0) return AA_ERR_SHAPE;
   if (B == 0) return AA_OK;
   if (!feats || !a_g || !V || !v_g || !h0 || !c0) return AA_ERR_NULL;
-  if (!al16(feats) || !al16(a_g) || !al16(V) || !al16(VWv)) return AA_ERR_ALIGN;
-  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, (hipStream_t)stream);
+  if (!al16(feats) || !al16(a_g) || !al16(V) || !al16(VWv) || !al16(v_g)) return AA_ERR_ALIGN;
+  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, nullptr, (hipStream_t)stream);
 }
 
 // ---- workspace carving ----------------------------------------------------------------------
@@ -676,22 +1006,26 @@ struct Carver {
 };
 
 struct StepWS {
-  float *sx, *u, *vwv;
+  float *xg, *s, *u, *vwv, *part;
   uint64_t* keys;
 };
 static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
   Carver c{base};
   StepWS w;
-  w.sx = c.take<float>((size_t)B * L.H);
+  w.xg = c.take<float>((size_t)B * L.N5);
+  w.s = c.take<float>((size_t)B * L.H);
   w.u = c.take<float>((size_t)B * L.H);
   w.vwv = c.take<float>((size_t)B * P * PP);
+  w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
   w.keys = c.take<uint64_t>((size_t)B);
   *bytes = c.off;
   return w;
 }
 
 struct DecodeWS {
-  float *a_g, *V, *vwv, *vg, *h[2], *c[2], *sx, *u;
+  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part;
+  uint16_t* ub;
+  float4* summ;
   uint64_t* keys;
 };
 static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* bytes) {
@@ -701,12 +1035,17 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.V = c.take<float>((size_t)B * P * L.H);
   w.vwv = c.take<float>((size_t)B * P * PP);
   w.vg = c.take<float>((size_t)B * L.E);
+  w.xg = c.take<float>((size_t)B * L.N5);
   for (int i = 0; i < 2; ++i) {
     w.h[i] = c.take<float>((size_t)B * L.H);
     w.c[i] = c.take<float>((size_t)B * L.H);
   }
-  w.sx = c.take<float>((size_t)B * L.H);
+  w.s = c.take<float>((size_t)B * L.H);
   w.u = c.take<float>((size_t)B * L.H);
+  w.unorm = c.take<float>((size_t)B);
+  w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
+  w.ub = c.take<uint16_t>((size_t)B * L.H);
+  w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
   *bytes = c.off;
   return w;
@@ -726,24 +1065,25 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
   return n;
 }
 
-static void step_launch(const Layout& L, const MP& p, int B, const uint64_t* keys_prev, const int64_t* tok_in,
-                        const float* V, const float* vwv, const float* vg, const float* h_in, const float* c_in,
-                        float* h_out, float* c_out, float* sx, float* u, float* alpha, int64_t alpha_ld, float* beta,
-                        int64_t beta_ld, float* scores, uint64_t* keys, const aa_trace* tr, int t, hipStream_t s) {
-  const int E = L.E, H = L.H, Vv = L.V;
-  const int MT = (B + 63) / 64;
-  if (tr && tr->lstm_events) (void)hipEventRecord((hipEvent_t)tr->lstm_events[2 * t], s);
-  hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16 + H / 64)), dim3(256), 0, s, B, E, H, Vv, keys_prev, tok_in, p.embed,
-                     vg, h_in, c_in, p.lstm_w, p.lstm_b, p.sent_w, h_out, c_out, sx);
-  if (tr && tr->lstm_events) (void)hipEventRecord((hipEvent_t)tr->lstm_events[2 * t + 1], s);
-  if (tr && tr->atten_events) (void)hipEventRecord((hipEvent_t)tr->atten_events[2 * t], s);
-  hipLaunchKernelGGL(k_atten, dim3(B), dim3(256), 0, s, B, H, h_out, c_out, sx, V, vwv, p.wg, p.ws, p.wh, alpha,
-                     alpha_ld, beta, beta_ld, u);
-  if (tr && tr->atten_events) (void)hipEventRecord((hipEvent_t)tr->atten_events[2 * t + 1], s);
-  if (tr && tr->vocab_events) (void)hipEventRecord((hipEvent_t)tr->vocab_events[2 * t], s);
-  hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 128)), dim3(256), 0, s, B, H, Vv, L.Vp, u, p.mlp_w, p.mlp_b, scores,
-                     keys);
-  if (tr && tr->vocab_events) (void)hipEventRecord((hipEvent_t)tr->vocab_events[2 * t + 1], s);
+static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
+  if (arr) (void)hipEventRecord((hipEvent_t)arr[i], s);
+}
+
+// LSTM + attention for one step (shared by the step API and the greedy loop)
+static void lstm_atten_launch(const Layout& L, const MP& p, int B, const uint64_t* keys_prev, const int64_t* tok_in,
+                              const float* V, const float* vwv, const float* xg, const float* h_in, const float* c_in,
+                              float* h_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
+                              float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
+                              const aa_trace* tr, int t, hipStream_t s) {
+  const int H = L.H, MT = (B + 63) / 64;
+  rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
+  hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16)), dim3(256), 0, s, B, H, L.V, keys_prev, tok_in, p.table, xg, h_in,
+                     c_in, p.whh, p.wg, p.ws, h_out, c_out, s_buf, part);
+  rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
+  rec(tr ? tr->atten_events : nullptr, 2 * t, s);
+  hipLaunchKernelGGL(k_atten, dim3(B), dim3(256), 0, s, B, H, H / 16, h_out, s_buf, part, V, vwv, p.wh, alpha,
+                     alpha_ld, beta, beta_ld, u, ub, unorm);
+  rec(tr ? tr->atten_events : nullptr, 2 * t + 1, s);
 }
 
 int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const float* V, const float* VWv,
@@ -765,18 +1105,22 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   hipStream_t s = (hipStream_t)stream;
   const MP p = resolve(m, L);
   if (!VWv) {
-    hipLaunchKernelGGL(k_vwv, dim3((B * P + 63) / 64), dim3(256), 0, s, V, B * P, L.H, p.wv, w.vwv);
+    gemm_bias(V, L.H, B * P, p.wv, L.H, PP, L.H, nullptr, w.vwv, PP, s);
     VWv = w.vwv;
   }
+  gemm_bias(v_g, L.E, B, p.wvg, L.E, L.N5, L.E, p.bias5, w.xg, L.N5, s);
   AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)B * sizeof(uint64_t), s));
-  step_launch(L, p, B, nullptr, tokens_in, V, VWv, v_g, h_in, c_in, h_out, c_out, w.sx, w.u, alpha, P, beta, 1, scores,
-              w.keys, nullptr, 0, s);
+  lstm_atten_launch(L, p, B, nullptr, tokens_in, V, VWv, w.xg, h_in, c_in, h_out, c_out, w.s, w.part, w.u, nullptr,
+                    nullptr, alpha, P, beta, 1, nullptr, 0, s);
+  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w,
+                     p.mlp_b, scores, w.keys);
   hipLaunchKernelGGL(k_finalize, dim3((B + 255) / 256), dim3(256), 0, s, w.keys, B, 1, tokens_out);
   return launch_status();
 }
 
 int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
-                     float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, aa_stream_t stream) {
+                     float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                     aa_stream_t stream) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
@@ -789,19 +1133,64 @@ int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   hipStream_t s = (hipStream_t)stream;
   const MP p = resolve(m, L);
-  AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
-  if (trace && trace->encoder_events) (void)hipEventRecord((hipEvent_t)trace->encoder_events[0], s);
-  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, s);
+  const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
+  if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
+  rec(trace ? trace->encoder_events : nullptr, 0, s);
+  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg, s);
   if (rc) return rc;
-  if (trace && trace->encoder_events) (void)hipEventRecord((hipEvent_t)trace->encoder_events[1], s);
+  rec(trace ? trace->encoder_events : nullptr, 1, s);
+  const int MT = (B + 63) / 64;
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
-    step_launch(L, p, B, t ? w.keys + (size_t)(t - 1) * B : nullptr, nullptr, w.V, w.vwv, w.vg, w.h[cur], w.c[cur],
-                w.h[nxt], w.c[nxt], w.sx, w.u, alpha ? alpha + (size_t)t * P : nullptr, (int64_t)T * P,
-                beta ? beta + t : nullptr, T, nullptr, w.keys + (size_t)t * B, trace, t, s);
+    lstm_atten_launch(L, p, B, t ? w.keys + (size_t)(t - 1) * B : nullptr, nullptr, w.V, w.vwv, w.xg, w.h[cur],
+                      w.c[cur], w.h[nxt], w.c[nxt], w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
+                      alpha ? alpha + (size_t)t * P : nullptr, (int64_t)T * P, beta ? beta + t : nullptr, T, trace, t, s);
+    uint64_t* kt = w.keys + (size_t)t * B;
+    rec(trace ? trace->vocab_events : nullptr, 2 * t, s);
+    if (exact) {
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
+                         nullptr, kt);
+    } else {
+      hipLaunchKernelGGL(k_vscreen, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.H, L.V,
+                         L.Vp, w.ub, w.unorm,
+                         p.mlp_wb, p.mlp_wn, p.mlp_b, w.summ);
+      hipLaunchKernelGGL(k_vrescore, dim3(B), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
+                         ids, T, t);
+    }
+    rec(trace ? trace->vocab_events : nullptr, 2 * t + 1, s);
   }
-  const int64_t n = (int64_t)B * T;
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.keys, B, T, ids);
+  if (exact) {
+    const int64_t n = (int64_t)B * T;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.keys, B, T, ids);
+  }
+  return launch_status();
+}
+
+int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* scores, aa_stream_t stream) {
+  Layout L;
+  int rc = check_model(m, &L);
+  if (rc) return rc;
+  if (B < 0) return AA_ERR_SHAPE;
+  if (B == 0) return AA_OK;
+  if (!u || !scores) return AA_ERR_NULL;
+  if (!al16(u)) return AA_ERR_ALIGN;
+  const MP p = resolve(m, L);
+  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, (hipStream_t)stream, B, L.H, L.V, L.Vp,
+                     u, p.mlp_w, p.mlp_b, scores, nullptr);
+  return launch_status();
+}
+
+int aa_vocab_logits_at(const aa_model* m, int32_t B, const float* u, const int32_t* cols, int32_t n, float* out,
+                       aa_stream_t stream) {
+  Layout L;
+  int rc = check_model(m, &L);
+  if (rc) return rc;
+  if (B < 0 || n < 0) return AA_ERR_SHAPE;
+  if (B == 0 || n == 0) return AA_OK;
+  if (!u || !cols || !out) return AA_ERR_NULL;
+  if (!al16(u)) return AA_ERR_ALIGN;
+  const MP p = resolve(m, L);
+  hipLaunchKernelGGL(k_logits_at, dim3(B), dim3(256), 0, (hipStream_t)stream, L.H, L.V, u, cols, n, p.mlp_w, p.mlp_b, out);
   return launch_status();
 }
 
@@ -815,4 +1204,3 @@ int aa_synth_uniform(float* dst, int64_t n, uint64_t key, int64_t start, double 
                      (hipStream_t)stream, dst, n, key, start, lo, hi - lo, plain);
   return launch_status();
 }
-

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 1
+#define AA_ABI_VERSION 2
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -46,7 +46,7 @@ typedef void* aa_event_t;  /* hipEvent_t */
 
 /* Model dimensions: cf.adaptive_word_embed_size, cf.adaptive_lstm_hidden_size, cf.vocab_length
  * (code_src/config/cfg_wzn.py:115-116, code_src/train.py:40), ResNet channels and 7x7 locations.
- * Supported: embed % 32 == 0, hidden % 128 == 0 and <= 1024, vocab >= 1, channels % 32 == 0,
+ * Supported: embed % 32 == 0, hidden % 256 == 0 and <= 1024, vocab >= 1, channels % 32 == 0,
  * spatial == 49. */
 typedef struct aa_dims {
   int32_t embed;    /* E = 256 */
@@ -137,13 +137,34 @@ AA_API int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in
 /* Workspace for aa_greedy_decode at batch B and T steps. */
 AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
 
+/* Decode flags */
+#define AA_DECODE_EXACT_VOCAB 1 /* compute every fp32 logit (fp32 MFMA GEMM + fused argmax) instead of
+                                   the bf16 screen + exact fp32 rescoring; both give the same ids */
+
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];
  * ids [B,T] int64; alpha [B,T,P] and beta [B,T] may be NULL.  All T steps run (no early stop),
- * the first input token is <start> = 1.  trace may be NULL. */
+ * the first input token is <start> = 1.  trace may be NULL.
+ * Vocab argmax (adaptive_attention.py:201): by default every logit is first bounded with a bf16
+ * MFMA screen whose error is bounded rigorously (|bf16 logit - fp32 logit| <= 0.0085 ||u|| ||w_n||);
+ * only columns whose upper bound reaches the best lower bound are rescored in exact fp32 (the same
+ * fma order as the fp32 GEMM), so the ids equal those of AA_DECODE_EXACT_VOCAB bit for bit. */
 AA_API int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T,
                             int64_t* ids, float* alpha, float* beta, void* workspace,
-                            size_t workspace_bytes, const aa_trace* trace, aa_stream_t stream);
+                            size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                            aa_stream_t stream);
+
+/* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
+ * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */
+AA_API int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* scores,
+                           aa_stream_t stream);
+
+/* Exact fp32 vocab logits of selected columns: out[b][i] = u[b] . W_m[cols[b][i]] + b_m[cols[b][i]]
+ * (AdaptiveBlock.mlp, adaptive_attention.py:132), computed in the fma order of the fp32 GEMM path,
+ * i.e. bit-identical to the corresponding aa_decode_step scores.  u [B,H]; cols [B,n] int32
+ * (entries outside [0, vocab) give 0); out [B,n].  Used to rescore candidate tokens. */
+AA_API int aa_vocab_logits_at(const aa_model* m, int32_t B, const float* u, const int32_t* cols,
+                              int32_t n, float* out, aa_stream_t stream);
 
 /* Counter-based synthetic data (same bits as adaptive_amd/synth.py):
  * dst[i] = fp32(lo + (hi - lo) * u(key, start + i)), u = (splitmix64(key + (start+i+1)*GOLDEN) >> 40) / 2^24.

@@ -42,12 +42,13 @@ def test_dims_and_sizes(lib):
     d = _lib.Dims(256, 512, 10123, 2048, 49)
     assert lib.aa_abi_version() == _lib.ABI_VERSION
     assert lib.aa_check_dims(d) == 0
-    assert lib.aa_check_dims(_lib.Dims(256, 500, 10123, 2048, 49)) == -2   # hidden % 128
+    assert lib.aa_check_dims(_lib.Dims(256, 500, 10123, 2048, 49)) == -2   # hidden % 256
+    assert lib.aa_check_dims(_lib.Dims(256, 384, 10123, 2048, 49)) == -2
     assert lib.aa_check_dims(_lib.Dims(256, 512, 10123, 2048, 36)) == -2   # spatial must be 49
     assert lib.aa_packed_bytes(_lib.Dims(256, 500, 10123, 2048, 49)) == 0
     pk = lib.aa_packed_bytes(d)
-    # packed weights: ~55.8 MB (encoder tail + decoder incl. the 10.4 MB embedding table, padded)
-    assert 55e6 < pk < 57e6
+    # packed weights: encoder tail + decoder + the 104 MB per-token LSTM-input table + bf16 W_m copy
+    assert 150e6 < pk < 170e6
     ws = lib.aa_decode_workspace_bytes(d, 512, 20)
     assert ws > 512 * 49 * 512 * 4  # holds V
     assert lib.aa_decode_workspace_bytes(d, 0, 20) == 0
@@ -56,15 +57,15 @@ def test_dims_and_sizes(lib):
 
 def test_argument_errors_without_device_work(lib):
     from adaptive_amd import _lib
-    assert lib.aa_greedy_decode(None, None, 1, 1, None, None, None, None, 0, None, None) == -1
+    assert lib.aa_greedy_decode(None, None, 1, 1, None, None, None, None, 0, None, 0, None) == -1
     m = _lib.Model(_lib.Dims(256, 512, 10123, 2048, 49), 256, 10)  # fake aligned pointer, too small
-    assert lib.aa_greedy_decode(m, None, 1, 1, None, None, None, None, 0, None, None) == -4
+    assert lib.aa_greedy_decode(m, None, 1, 1, None, None, None, None, 0, None, 0, None) == -4
     m = _lib.Model(_lib.Dims(256, 512, 10123, 2048, 49), 256 + 16, 10 ** 9)
-    assert lib.aa_greedy_decode(m, None, 1, 1, None, None, None, None, 0, None, None) == -5  # 256-B alignment
+    assert lib.aa_greedy_decode(m, None, 1, 1, None, None, None, None, 0, None, 0, None) == -5  # 256-B alignment
     m = _lib.Model(_lib.Dims(256, 512, 10123, 2048, 49), 256, 10 ** 9)
-    assert lib.aa_greedy_decode(m, None, -1, 1, None, None, None, None, 0, None, None) == -3
-    assert lib.aa_greedy_decode(m, None, 0, 20, None, None, None, None, 0, None, None) == 0   # empty batch
-    assert lib.aa_greedy_decode(m, None, 4, 20, None, None, None, None, 0, None, None) == -1
+    assert lib.aa_greedy_decode(m, None, -1, 1, None, None, None, None, 0, None, 0, None) == -3
+    assert lib.aa_greedy_decode(m, None, 0, 20, None, None, None, None, 0, None, 0, None) == 0   # empty batch
+    assert lib.aa_greedy_decode(m, None, 4, 20, None, None, None, None, 0, None, 0, None) == -1
     assert b"too small" in lib.aa_error_string(-4)
 
 

@@ -187,3 +187,29 @@ def test_errors_are_loud(model, gpu_device):
     with pytest.raises(IndexError):
         V, v_g, st, _, _ = model._encode(torch.from_numpy(synth.make_features(2)).to(gpu_device))
         model.decoder(V, v_g, torch.full((2, 1), 10123, dtype=torch.int64, device=gpu_device), st)
+
+
+def test_rescoring_logits_bit_identical_to_fp32_gemm(model, gpu_device):
+    """The exact-fp32 rescoring (used after the bf16 screen) reproduces the fp32 MFMA GEMM's logits
+    bit for bit (same fma order), so screening never changes which column wins a near-tie."""
+    g = torch.Generator().manual_seed(0)
+    u = (torch.rand(77, 512, generator=g) * 2 - 1).to(gpu_device)
+    full = model.vocab_logits(u)
+    cols = torch.randint(0, 10123, (77, 300), generator=g).to(gpu_device)
+    cols[:, 0] = 10122
+    cols[:, 1] = 0
+    part = model.vocab_logits(u, cols)
+    assert torch.equal(part, torch.gather(full, 1, cols.long()))
+    ref = u.cpu() @ model.decoder.adaptive.mlp.weight.detach().cpu().T + model.decoder.adaptive.mlp.bias.detach().cpu()
+    np.testing.assert_allclose(full.cpu().numpy(), ref.numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("seed,noise,fseed,B,T", [(123, 0.0, 0, 512, 20), (99, 0.02, 7, 300, 20), (5, 0.0, 3, 64, 30)])
+def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device):
+    """bf16 screen + exact rescoring == full fp32 logits argmax, token for token."""
+    m = _model(seed, noise)
+    feats = torch.from_numpy(synth.make_features(B, seed=fseed)).to(gpu_device)
+    a = m.sampler(feats, max_len=T)
+    b = m.sampler(feats, max_len=T, exact_vocab=True)
+    assert torch.equal(a[0], b[0])
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
