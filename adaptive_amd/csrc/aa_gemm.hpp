@@ -84,11 +84,13 @@ struct WRowMajor {
 };
 
 // Main loop: accumulates k-steps [0, nk) of the tile into acc.  `lds` holds Tile::LDS_FLOATS.
+// `tid` is the thread's index inside its 256-thread group and `ks0` the first K-step, so a
+// 512-thread workgroup can run two groups over the two halves of K (each with its own `lds`).
 template <int BM, int BN, class AL, class WL>
 __device__ __forceinline__ void gemm_mainloop(const AL& al, const WL& wl, int nk, float* lds,
-                                              floatx16 (&acc)[BM / 64][BN / 64]) {
+                                              floatx16 (&acc)[BM / 64][BN / 64], int tid = -1, int ks0 = 0) {
   using T = Tile<BM, BN>;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = tid < 0 ? (int)threadIdx.x : tid, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
 #pragma unroll
@@ -101,9 +103,9 @@ __device__ __forceinline__ void gemm_mainloop(const AL& al, const WL& wl, int nk
   float4 ra[T::AF4], rw[T::WF4];
   auto gload = [&](int ks) {
 #pragma unroll
-    for (int i = 0; i < T::AF4; ++i) ra[i] = al.load(i, t + NT * i, ks * BK);
+    for (int i = 0; i < T::AF4; ++i) ra[i] = al.load(i, t + NT * i, (ks0 + ks) * BK);
 #pragma unroll
-    for (int i = 0; i < T::WF4; ++i) rw[i] = wl.load(t + NT * i, ks * BK);
+    for (int i = 0; i < T::WF4; ++i) rw[i] = wl.load(t + NT * i, (ks0 + ks) * BK);
   };
   auto lstore = [&](int buf) {
     float* As = lds + buf * T::STAGE;

@@ -63,7 +63,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn;
+  size_t enc_a_w, enc_a_b, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, wgs;
   size_t total_floats;
 };
 
@@ -95,13 +95,14 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_b = take(L.Vp);
   L.mlp_wb = take((size_t)L.Vp * L.H / 2);  // bf16
   L.mlp_wn = take(L.Vp);
+  L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
-      *mlp_b, *mlp_wn;
+      *mlp_b, *mlp_wn, *wgs;
   const uint16_t* mlp_wb;
 };
 
@@ -113,7 +114,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
   p.mlp_w = b + L.mlp_w; p.mlp_b = b + L.mlp_b;
-  p.mlp_wb = reinterpret_cast<const uint16_t*>(b + L.mlp_wb); p.mlp_wn = b + L.mlp_wn;
+  p.mlp_wb = reinterpret_cast<const uint16_t*>(b + L.mlp_wb); p.mlp_wn = b + L.mlp_wn; p.wgs = b + L.wgs;
   return p;
 }
 
@@ -304,39 +305,56 @@ __global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, 
 // ---------------------------------------------------------------------------------------------
 constexpr int PART = 128;  // partial-projection row pitch (2 x 49 used)
 
-__global__ __launch_bounds__(256) void k_lstm(int B, int H, int V, const uint64_t* __restrict__ keys_prev,
+// 512 threads: two groups of 4 waves run the two halves of K (each its own double-buffered LDS),
+// group 1's accumulators are added to group 0's in a fixed order (g0 + g1), then the epilogue.
+__global__ __launch_bounds__(512) void k_lstm(int B, int H, int V, const uint64_t* __restrict__ keys_prev,
                                               const int64_t* __restrict__ tok_in, const float* __restrict__ table,
                                               const float* __restrict__ xg, const float* __restrict__ h_in,
                                               const float* __restrict__ c_in, const float* __restrict__ whh,
-                                              const float* __restrict__ Wg, const float* __restrict__ Ws,
-                                              float* __restrict__ h_out, float* __restrict__ c_out, float* __restrict__ s_out,
+                                              const float* __restrict__ wgs, float* __restrict__ h_out,
+                                              float* __restrict__ c_out, float* __restrict__ s_out,
                                               float* __restrict__ part) {
   constexpr int BM = 64, BN = 64;
-  __shared__ __attribute__((aligned(16))) float lds[Tile<BM, BN>::LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[2 * Tile<BM, BN>::LDS_FLOATS];
   const int MT = (B + BM - 1) / BM, NTn = H / 16;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int t = threadIdx.x, grp = t >> 8, tg = t & 255;
+  const int lane = t & 63, wave = tg >> 6, wm = wave >> 1, wn = wave & 1;
   const int m0 = mt * BM;
+  const int nkh = H / BK / 2;
   ARowMajor al{h_in, H, m0, B};
   WRowMajor wl{whh, H, nt * BN};
   floatx16 acc[1][1];
-  gemm_mainloop<BM, BN>(al, wl, H / BK, lds, acc);
+  gemm_mainloop<BM, BN>(al, wl, nkh, lds + grp * Tile<BM, BN>::LDS_FLOATS, acc, tg, grp * nkh);
   constexpr int CP = 68;
   float* Cs = lds;                 // [64][CP] gate pre-activations
-  float* Hs = lds + 64 * CP;       // [64][16] h' of the tile
+  float* C1 = Cs + 64 * CP;        // [64][CP] group-1 partial sums
+  float* Hs = C1 + 64 * CP;        // [64][16] h' of the tile
   float* Ss = Hs + 64 * 16;        // [64][16] s of the tile
-  float* Wsl = Ss + 64 * 16;       // [98][17] W_g / W_s columns of the tile's units (padded: no bank conflicts)
+  float* Wsl = Ss + 64 * 16;       // [98][17] W_g / W_s columns of the tile's units (padded)
+  if (grp == 1) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) Cs[(wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31)] = acc[0][0][r];
-  for (int i = t; i < 2 * P * 16; i += 256) {  // 98 rows x 16 units
-    const int j = i >> 4, u = i & 15;
-    const float* src = j < P ? Wg + (int64_t)j * H : Ws + (int64_t)(j - P) * H;
-    Wsl[j * 17 + u] = src[nt * 16 + u];
+    for (int r = 0; r < 16; ++r) C1[(wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31)] = acc[0][0][r];
+  } else {
+    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+    for (int i = tg; i < 2 * P * 4; i += 256) {
+      const float4 v = src[i];
+      float* d = Wsl + (i >> 2) * 17 + 4 * (i & 3);
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
   }
   __syncthreads();
-  const int rr = t >> 2, u0 = (t & 3) * 4, m = m0 + rr;
-  {
+  if (grp == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int idx = (wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31);
+      Cs[idx] = acc[0][0][r] + C1[idx];
+    }
+  }
+  __syncthreads();
+  if (grp == 0) {
+    const int rr = tg >> 2, u0 = (tg & 3) * 4, m = m0 + rr;
     const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
     int64_t tk = 1;  // <start> (adaptive_attention.py:187-190)
     if (keys_prev) tk = key_token(keys_prev[mc]);
@@ -379,14 +397,14 @@ __global__ __launch_bounds__(256) void k_lstm(int B, int H, int V, const uint64_
     }
   }
   __syncthreads();
-  // partial projections: thread -> j = t % 128 (valid < 98), rows t/128, t/128 + 2, ...
+  // partial projections: thread -> j = t % 128 (valid < 98), rows t/128, t/128 + 4, ...
   const int jp = t & 127;
   if (jp < 2 * P) {
     float w[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) w[u] = Wsl[jp * 17 + u];
     const float* vals = jp < P ? Hs : Ss;
-    for (int r = t >> 7; r < BM; r += 2) {
+    for (int r = t >> 7; r < BM; r += 4) {
       const int mr = m0 + r;
       if (mr >= B) break;
       float a = 0.f;
@@ -405,13 +423,18 @@ __global__ __launch_bounds__(256) void k_lstm(int B, int H, int V, const uint64_
 //   c_t   = sum_k alpha_k V[k];  u = beta s + (1 - beta) c_t + h_t       (:42, :56, :132)
 // Also emits bf16(u) and ||u||_2 for the vocab screen.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_atten(int B, int H, int NTL, const float* __restrict__ h_new,
+// Latency structure: every load that does not depend on alpha is issued up front (this thread's V
+// columns, VWv scores operands, h, s, the partial projections), so the kernel pays ~one memory
+// latency instead of one per phase.  HPT = H / 256 columns per thread.
+template <int HPT>
+__global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __restrict__ h_new,
                                                const float* __restrict__ s_new, const float* __restrict__ part,
                                                const float* __restrict__ Vf, const float* __restrict__ VWv,
                                                const float* __restrict__ wh, float* __restrict__ alpha_out,
                                                int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
                                                float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
                                                float* __restrict__ unorm) {
+  constexpr int H = 256 * HPT;
   __shared__ float proj[PART];
   __shared__ float zs[PP];
   __shared__ float sh_alpha[PP];
@@ -419,29 +442,60 @@ __global__ __launch_bounds__(256) void k_atten(int B, int H, int NTL, const floa
   __shared__ float sh_norm[4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = blockIdx.x;
-  // 1) projections: fixed tile order
-  if (t < 2 * P) {
-    const float* pp = part + (int64_t)b * NTL * PART + t;
+  // ---- loads independent of alpha, oldest first in the order they are consumed ------------------
+  // (vmcnt retires in issue order: the partial sums wait only for the partials, the scores only
+  //  for partials + VWv, while the 98 V values of this thread stay in flight.)  No branches
+  //  around loads: out-of-range lanes read clamped addresses and their values are never used.
+  constexpr int NT16 = H / 16;  // == NTL
+  const int tp = t < 2 * P ? t : 2 * P - 1;
+  float pv[NT16];
+  {
+    const float* pp = part + (int64_t)b * NT16 * PART + tp;
+#pragma unroll
+    for (int i = 0; i < NT16; ++i) pv[i] = pp[(int64_t)i * PART];
+  }
+  const int k = t >> 2, q = t & 3;
+  const int kc = k < P ? k : P - 1;
+  const float* vw = VWv + ((int64_t)b * P + kc) * PP;
+  float vwr[13], whr[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int j = q + 4 * i < P ? q + 4 * i : P - 1;
+    vwr[i] = vw[j];
+    whr[i] = q + 4 * i < P ? wh[j] : 0.f;  // w_h = 0 for the padding term: fma(0, tanh(.), z) == z
+  }
+  const float* vb = Vf + (int64_t)b * P * H;
+  float vv[HPT][P];
+#pragma unroll
+  for (int i = 0; i < HPT; ++i)
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 256 * i];
+  float hv[HPT], sv[HPT];
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    hv[i] = h_new[(int64_t)b * H + t + 256 * i];
+    sv[i] = s_new[(int64_t)b * H + t + 256 * i];
+  }
+  // 1) projections: partials of the H/16 LSTM tiles added in fixed tile order
+  {
     float a = 0.f;
-    for (int i = 0; i < NTL; ++i) a += pp[(int64_t)i * PART];
-    proj[t] = a;
+#pragma unroll
+    for (int i = 0; i < NT16; ++i) a += pv[i];
+    if (t < 2 * P) proj[t] = a;
   }
   __syncthreads();
-  // 2) scores: item k (0..49) by a quad of lanes, j strided by 4, quad combined in fixed order
+  // 2) scores: item k (0..49) by a quad of lanes, j = q + 4i, quad combined in fixed order
   {
-    const int k = t >> 2, q = t & 3;
     float z = 0.f;
-    if (k <= P) {
-      const float* vw = VWv + ((int64_t)b * P + k) * PP;
-      for (int j = q; j < P; j += 4) {
-        const float x = (k < P ? vw[j] : proj[P + j]) + proj[j];
-        z = __builtin_fmaf(wh[j], tanhf(x), z);
-      }
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      const int j = q + 4 * i < P ? q + 4 * i : P - 1;
+      const float x = (k < P ? vwr[i] : proj[P + j]) + proj[j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
     }
     const float z1 = __shfl_xor(z, 1, 64);
     const float z2 = __shfl_xor(z, 2, 64);
     const float z3 = __shfl_xor(z, 3, 64);
-    // lane q0 of the quad holds s0; (s0 + s1) + (s2 + s3) in a fixed association
     if (q == 0 && k <= P) zs[k] = (z + z1) + (z2 + z3);
   }
   __syncthreads();
@@ -470,14 +524,15 @@ __global__ __launch_bounds__(256) void k_atten(int B, int H, int NTL, const floa
   __syncthreads();
   // 4) context + u
   const float beta = sh_beta;
-  const float* vb = Vf + (int64_t)b * P * H;
   float nsq = 0.f;
-  for (int d = t; d < H; d += 256) {
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int d = t + 256 * i;
     float c = 0.f;
-#pragma unroll 7
-    for (int k = 0; k < P; ++k) c = __builtin_fmaf(sh_alpha[k], vb[(int64_t)k * H + d], c);
-    const float chat = __builtin_fmaf(beta, s_new[(int64_t)b * H + d], (1.f - beta) * c);
-    const float u = chat + h_new[(int64_t)b * H + d];
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sh_alpha[kk], vv[i][kk], c);
+    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
+    const float u = chat + hv[i];
     nsq = __builtin_fmaf(u, u, nsq);
     u_out[(int64_t)b * H + d] = u;
     if (ub_out) ub_out[(int64_t)b * H + d] = f2bf(u);
@@ -829,6 +884,16 @@ __global__ void k_pack_lstm(const float* __restrict__ w_ih, const float* __restr
   }
 }
 
+// wgs[tile][j][u] = (j < 49 ? W_g[j] : W_s[j - 49])[tile*16 + u]
+__global__ void k_pack_wgs(const float* __restrict__ wg, const float* __restrict__ ws, int H, float* __restrict__ out) {
+  const int tile = blockIdx.x;
+  for (int i = threadIdx.x; i < 2 * P * 16; i += blockDim.x) {
+    const int j = i / 16, u = i % 16;
+    const float* src = j < P ? wg + (int64_t)j * H : ws + (int64_t)(j - P) * H;
+    out[(int64_t)tile * 2 * P * 16 + i] = src[tile * 16 + u];
+  }
+}
+
 // bf16 copy of W_m (zero rows beyond V) and inflated row norms ||w_n||_2 for the screen bound.
 __global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, uint16_t* __restrict__ wb, float* __restrict__ wn) {
   const int n = blockIdx.x, lane = threadIdx.x;  // 64 threads
@@ -959,6 +1024,7 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   gemm_bias(w->embed_w, E, V, base + L.wemb, E, L.N5, E, nullptr, base + L.table, L.N5, s);
   hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H,
                      reinterpret_cast<uint16_t*>(base + L.mlp_wb), base + L.mlp_wn);
+  hipLaunchKernelGGL(k_pack_wgs, dim3(H / 16), dim3(256), 0, s, w->att_affine_g_w, w->att_affine_s_w, H, base + L.wgs);
   return launch_status();
 }
 
@@ -1077,12 +1143,20 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const uint64_
                               const aa_trace* tr, int t, hipStream_t s) {
   const int H = L.H, MT = (B + 63) / 64;
   rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
-  hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16)), dim3(256), 0, s, B, H, L.V, keys_prev, tok_in, p.table, xg, h_in,
-                     c_in, p.whh, p.wg, p.ws, h_out, c_out, s_buf, part);
+  hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16)), dim3(512), 0, s, B, H, L.V, keys_prev, tok_in, p.table, xg, h_in,
+                     c_in, p.whh, p.wgs, h_out, c_out, s_buf, part);
   rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
   rec(tr ? tr->atten_events : nullptr, 2 * t, s);
-  hipLaunchKernelGGL(k_atten, dim3(B), dim3(256), 0, s, B, H, H / 16, h_out, s_buf, part, V, vwv, p.wh, alpha,
-                     alpha_ld, beta, beta_ld, u, ub, unorm);
+#define AA_ATTEN(HPT_)                                                                                     \
+  hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, h_out, s_buf, part, V, vwv, p.wh, alpha, \
+                     alpha_ld, beta, beta_ld, u, ub, unorm)
+  switch (H / 256) {
+    case 1: AA_ATTEN(1); break;
+    case 2: AA_ATTEN(2); break;
+    case 3: AA_ATTEN(3); break;
+    default: AA_ATTEN(4); break;
+  }
+#undef AA_ATTEN
   rec(tr ? tr->atten_events : nullptr, 2 * t + 1, s);
 }
 
