@@ -15,7 +15,7 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 DECODE_EXACT_VOCAB = 1
 
 
@@ -57,9 +57,12 @@ class Model(Structure):
     _fields_ = [("dims", Dims), ("packed", c_void_p), ("packed_bytes", c_size_t)]
 
 
+TRACE_ENCODER_KERNELS = 5  # k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM
+
+
 class Trace(Structure):
-    _fields_ = [("vocab_events", c_void_p), ("lstm_events", c_void_p), ("atten_events", c_void_p),
-                ("encoder_events", c_void_p)]
+    _fields_ = [("encoder_events", c_void_p), ("lstm_events", c_void_p), ("atten_events", c_void_p),
+                ("screen_events", c_void_p), ("rescore_events", c_void_p)]
 
 
 # name -> (restype, argtypes); mirrors include/adaptive_amd.h one to one

@@ -1028,22 +1028,36 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   return launch_status();
 }
 
+static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
+  if (arr) (void)hipEventRecord((hipEvent_t)arr[i], s);
+}
+
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
-                          float* h0, float* c0, float* VWv, float* xg, hipStream_t s) {
+                          float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, hipStream_t s) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
+  rec(ev, 0, s);
   hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, feats, nch, a_g);
+  rec(ev, 1, s);
+  rec(ev, 2, s);
   {
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
   }
+  rec(ev, 3, s);
+  rec(ev, 4, s);
   {
     const int MT = (B + 63) / 64, NTn = L.NHp / 64;
     hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, s, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
                        v_g, h0, c0);
   }
+  rec(ev, 5, s);
+  rec(ev, 6, s);
   if (VWv) gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
+  rec(ev, 7, s);
+  rec(ev, 8, s);
   if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, s);
+  rec(ev, 9, s);
   return launch_status();
 }
 
@@ -1056,7 +1070,7 @@ int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g
   if (B == 0) return AA_OK;
   if (!feats || !a_g || !V || !v_g || !h0 || !c0) return AA_ERR_NULL;
   if (!al16(feats) || !al16(a_g) || !al16(V) || !al16(VWv) || !al16(v_g)) return AA_ERR_ALIGN;
-  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, nullptr, (hipStream_t)stream);
+  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, nullptr, nullptr, (hipStream_t)stream);
 }
 
 // ---- workspace carving ----------------------------------------------------------------------
@@ -1131,9 +1145,6 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
   return n;
 }
 
-static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
-  if (arr) (void)hipEventRecord((hipEvent_t)arr[i], s);
-}
 
 // LSTM + attention for one step (shared by the step API and the greedy loop)
 static void lstm_atten_launch(const Layout& L, const MP& p, int B, const uint64_t* keys_prev, const int64_t* tok_in,
@@ -1209,10 +1220,9 @@ int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T
   const MP p = resolve(m, L);
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
-  rec(trace ? trace->encoder_events : nullptr, 0, s);
-  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg, s);
+  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
+                      trace ? trace->encoder_events : nullptr, s);
   if (rc) return rc;
-  rec(trace ? trace->encoder_events : nullptr, 1, s);
   const int MT = (B + 63) / 64;
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
@@ -1220,18 +1230,23 @@ int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T
                       w.c[cur], w.h[nxt], w.c[nxt], w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
                       alpha ? alpha + (size_t)t * P : nullptr, (int64_t)T * P, beta ? beta + t : nullptr, T, trace, t, s);
     uint64_t* kt = w.keys + (size_t)t * B;
-    rec(trace ? trace->vocab_events : nullptr, 2 * t, s);
+    aa_event_t* sev = trace ? trace->screen_events : nullptr;
+    aa_event_t* rev = trace ? trace->rescore_events : nullptr;
+    rec(sev, 2 * t, s);
     if (exact) {
       hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
                          nullptr, kt);
+      rec(sev, 2 * t + 1, s);
     } else {
       hipLaunchKernelGGL(k_vscreen, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.H, L.V,
                          L.Vp, w.ub, w.unorm,
                          p.mlp_wb, p.mlp_wn, p.mlp_b, w.summ);
+      rec(sev, 2 * t + 1, s);
+      rec(rev, 2 * t, s);
       hipLaunchKernelGGL(k_vrescore, dim3(B), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
                          ids, T, t);
+      rec(rev, 2 * t + 1, s);
     }
-    rec(trace ? trace->vocab_events : nullptr, 2 * t + 1, s);
   }
   if (exact) {
     const int64_t n = (int64_t)B * T;

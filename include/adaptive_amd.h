@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 2
+#define AA_ABI_VERSION 3
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -90,14 +90,20 @@ typedef struct aa_model {
   size_t packed_bytes;
 } aa_model;
 
-/* Optional per-kernel timing (hipEvent_t handles created by the caller).  For each non-NULL array,
- * aa_greedy_decode records event [2t] before and [2t+1] after the corresponding launch of step t
- * (2*T events each); encoder_events gets 2 events around the encoder tail. */
+/* Optional per-kernel timing (hipEvent_t handles created by the caller), one array per kernel so
+ * the averages line up with rocprofv3's per-kernel statistics.  For each non-NULL array,
+ * aa_greedy_decode records event [2i] before and [2i+1] after the i-th launch of that kernel:
+ *   encoder_events: 2*AA_TRACE_ENCODER_KERNELS events, launches in the order
+ *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
+ *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen
+ *                   (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused then). */
+#define AA_TRACE_ENCODER_KERNELS 5
 typedef struct aa_trace {
-  aa_event_t* vocab_events;
+  aa_event_t* encoder_events;
   aa_event_t* lstm_events;
   aa_event_t* atten_events;
-  aa_event_t* encoder_events; /* 2 events around the encoder tail (may be NULL) */
+  aa_event_t* screen_events;
+  aa_event_t* rescore_events;
 } aa_trace;
 
 AA_API int aa_abi_version(void);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box driver: every GPU step under its own timeout; stop at the first crash/timeout.
-# usage: bash run_gpu.sh <step>...   steps: smoke tests bench prof
+# usage: bash run_gpu.sh <step>...   steps: smoke tests testsall bench benchq prof pmc
 set -u
 mkdir -p gpurun_out
 ok_or_fail() {  # continue on 0 (pass) or 1 (test failures); stop on crashes/timeouts
@@ -17,6 +17,8 @@ for step in "$@"; do
     benchq) timeout -k 10 600 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-trace --steps 10 > gpurun_out/prof.log 2>&1; ok_or_fail $? prof ;;
+    pmc)  bash tools/pmc.sh traffic fetch write; ok_or_fail $? pmc
+          python tools/pmc_summary.py gpurun_out/pmc_traffic --traffic gpurun_out/traffic.json > gpurun_out/pmc_traffic/summary.txt 2>&1; cat gpurun_out/pmc_traffic/summary.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
