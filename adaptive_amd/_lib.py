@@ -17,6 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
 ABI_VERSION = 3
 DECODE_EXACT_VOCAB = 1
+MAX_LANES = 8
 
 
 class Dims(Structure):
@@ -81,6 +82,13 @@ SIGNATURES = {
     "aa_decode_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
     "aa_greedy_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_size_t, POINTER(Trace), c_int32, c_void_p]),
+    "aa_greedy_decode_lanes": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, POINTER(Trace), c_int32, c_void_p, POINTER(c_void_p),
+                                       c_int32]),
+    "aa_decode_plan_create": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_size_t, c_int32, c_int32, POINTER(c_void_p)]),
+    "aa_decode_plan_launch": (c_int, [c_void_p, c_void_p]),
+    "aa_decode_plan_destroy": (c_int, [c_void_p]),
     "aa_vocab_logits": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_void_p]),
     "aa_vocab_logits_at": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),

@@ -24,6 +24,9 @@ raises for B > 1) is not reproduced: the sampler uses the baseline's transpose s
 """
 from __future__ import annotations
 
+import collections
+import ctypes
+
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -153,8 +156,39 @@ class Decoder(nn.Module):
         return owner._decode_step(V, v_g, captions, states)
 
 
+class _Plan:
+    """An aa_decode_plan plus the buffers it was captured with (owned here, freed with it)."""
+
+    def __init__(self, lib, model, images, B, T, flags, n_lanes, cdims, dev):
+        self.lib = lib
+        self.images = images  # keep the captured input alive while the plan exists
+        self.ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+        self.alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+        self.beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+        nbytes = lib.aa_decode_workspace_bytes(cdims, B, T)
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            torch.cuda.current_stream().synchronize()  # buffers allocated above are ready
+            _lib.check(lib.aa_decode_plan_create(model, images.data_ptr(), B, T, self.ids.data_ptr(),
+                                                 self.alpha.data_ptr(), self.beta.data_ptr(), self.ws.data_ptr(),
+                                                 nbytes, flags, n_lanes, ctypes.byref(h)), "decode_plan_create")
+        self.handle = h
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize()
+            except Exception:
+                pass
+            self.lib.aa_decode_plan_destroy(h)
+
+
 class Encoder2Decoder(nn.Module):
     """adaptive_attention.Encoder2Decoder on MI355X kernels."""
+
+    MAX_PLANS = 4
 
     def __init__(self, cf):
         nn.Module.__init__(self)
@@ -167,6 +201,10 @@ class Encoder2Decoder(nn.Module):
         self._pack_key = None
         self._packed = None
         self._model = None
+        self.decode_lanes = 1  # HIP streams the greedy step loop is split over (sampler(lanes=...))
+        self.decode_graph = True  # replay repeated sampler calls from a captured hipGraph (aa_decode_plan)
+        self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
+        self._plan_seen = set()
 
     # ---- weights -------------------------------------------------------------------------------
     def load_synthetic(self, seed: int = 123, bias_noise: float = 0.0) -> "Encoder2Decoder":
@@ -211,6 +249,8 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             _lib.check(lib.aa_pack_weights(model, w, _lib.stream_handle()), "pack_weights")
         self._packed, self._model, self._pack_key = packed, model, key
+        self._plans.clear()  # plans bind the packed buffer
+        self._plan_seen.clear()
         return model
 
     def _check_images(self, images: torch.Tensor) -> torch.Tensor:
@@ -226,25 +266,66 @@ class Encoder2Decoder(nn.Module):
     # ---- Encoder2Decoder.sampler (adaptive_attention.py:168-216) --------------------------------
     @torch.no_grad()
     def sampler(self, images: torch.Tensor, max_len: int = 30, trace: Optional[_lib.Trace] = None,
-                exact_vocab: bool = False):
+                exact_vocab: bool = False, lanes: Optional[int] = None, graph: Optional[bool] = None):
         """Greedy decode -> (ids [B,max_len] int64, alpha [B,max_len,49], beta [B,max_len,1]).
 
         ``exact_vocab=True`` computes every fp32 logit; the default screens with bf16 under a rigorous
-        error bound and rescores the candidates in exact fp32 — the ids are identical."""
+        error bound and rescores the candidates in exact fp32 — the ids are identical.
+        ``lanes`` (default ``self.decode_lanes``) splits the step loop over that many HIP streams by
+        row blocks so the lanes' kernels overlap; captions are independent, results are identical.
+        ``graph`` (default ``self.decode_graph``): repeated calls on the same input buffer replay a
+        captured hipGraph of the whole decode (C-ABI aa_decode_plan); results are identical."""
         images = self._check_images(images)
         model = self._model_struct()
         lib = _lib.load()
         B, T, dev = images.size(0), int(max_len), images.device
+        n = int(self.decode_lanes if lanes is None else lanes)
+        if not 1 <= n <= _lib.MAX_LANES:
+            raise ValueError(f"lanes must be in [1, {_lib.MAX_LANES}], got {n}")
+        flags = _lib.DECODE_EXACT_VOCAB if exact_vocab else 0
+        use_graph = self.decode_graph if graph is None else bool(graph)
+        if use_graph and trace is None and B > 0 and T > 0:
+            # A plan binds the images pointer; it is captured the second time a key is seen, so
+            # one-off calls never pay for a capture.
+            key = (dev.index, images.data_ptr(), B, T, flags, n, self._packed.data_ptr())
+            plan = self._plans.get(key)
+            if plan is None and key in self._plan_seen:
+                plan = self._plans[key] = _Plan(lib, model, images, B, T, flags, n, self._c_dims(), dev)
+                while len(self._plans) > self.MAX_PLANS:
+                    self._plans.popitem(last=False)
+            if plan is not None:
+                self._plans.move_to_end(key)
+                with torch.cuda.device(dev):
+                    _lib.check(lib.aa_decode_plan_launch(plan.handle, _lib.stream_handle()), "decode_plan_launch")
+                return plan.ids.clone(), plan.alpha.clone(), plan.beta.clone()
+            if len(self._plan_seen) > 64:
+                self._plan_seen.clear()
+            self._plan_seen.add(key)
         ids = torch.empty(B, T, dtype=torch.int64, device=dev)
         alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
         beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
         ws = self._workspace(lib.aa_decode_workspace_bytes(self._c_dims(), B, T), dev)
         with torch.cuda.device(dev):
-            rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                      beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                      trace, _lib.DECODE_EXACT_VOCAB if exact_vocab else 0, _lib.stream_handle())
+            if n == 1:
+                rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                          beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                                          trace, flags, _lib.stream_handle())
+            else:
+                handles = (ctypes.c_void_p * n)(*[st.cuda_stream for st in self._lanes(n, dev)])
+                rc = lib.aa_greedy_decode_lanes(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                                beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                                                trace, flags, _lib.stream_handle(), handles, n)
         _lib.check(rc, "greedy_decode")
         return ids, alpha, beta
+
+    def _lanes(self, n: int, dev) -> list:
+        """n side streams on ``dev`` (created once, reused)."""
+        cache = self.__dict__.setdefault("_lane_streams", {})
+        key = (dev.index if dev.index is not None else torch.cuda.current_device())
+        have = cache.setdefault(key, [])
+        while len(have) < n:
+            have.append(torch.cuda.Stream(device=dev))
+        return have[:n]
 
     def _workspace(self, nbytes: int, dev) -> Optional[torch.Tensor]:
         if nbytes == 0:

@@ -1203,56 +1203,199 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   return launch_status();
 }
 
-int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
-                     float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
-                     aa_stream_t stream) {
+// The T-step loop over rows [r0, r0 + Bl) of the batch (every workspace array is row-indexed, so a
+// lane is the same loop on offset pointers; keys are [T][B]).
+static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, bool exact,
+                        int64_t* ids, float* alpha, float* beta, const aa_trace* trace, hipStream_t s) {
+  const int H = L.H, MT = (Bl + 63) / 64, NTn = L.Vp / VS_TILE;
+  const float* V = w.V + (size_t)r0 * P * H;
+  const float* vwv = w.vwv + (size_t)r0 * P * PP;
+  const float* xg = w.xg + (size_t)r0 * L.N5;
+  float* hb[2] = {w.h[0] + (size_t)r0 * H, w.h[1] + (size_t)r0 * H};
+  float* cb[2] = {w.c[0] + (size_t)r0 * H, w.c[1] + (size_t)r0 * H};
+  float* sb = w.s + (size_t)r0 * H;
+  float* part = w.part + (size_t)r0 * (H / 16) * PART;
+  float* u = w.u + (size_t)r0 * H;
+  uint16_t* ub = w.ub + (size_t)r0 * H;
+  float* unorm = w.unorm + r0;
+  float4* summ = w.summ + (size_t)r0 * NTn;
+  int64_t* idsl = ids + (size_t)r0 * T;
+  float* al = alpha ? alpha + (size_t)r0 * T * P : nullptr;
+  float* bl = beta ? beta + (size_t)r0 * T : nullptr;
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    const uint64_t* kprev = t ? w.keys + (size_t)(t - 1) * B + r0 : nullptr;
+    uint64_t* kt = w.keys + (size_t)t * B + r0;
+    lstm_atten_launch(L, p, Bl, kprev, nullptr, V, vwv, xg, hb[cur], cb[cur], hb[nxt], cb[nxt], sb, part, u,
+                      exact ? nullptr : ub, exact ? nullptr : unorm, al ? al + (size_t)t * P : nullptr,
+                      (int64_t)T * P, bl ? bl + t : nullptr, T, trace, t, s);
+    aa_event_t* sev = trace ? trace->screen_events : nullptr;
+    aa_event_t* rev = trace ? trace->rescore_events : nullptr;
+    rec(sev, 2 * t, s);
+    if (exact) {
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, p.mlp_w, p.mlp_b,
+                         nullptr, kt);
+      rec(sev, 2 * t + 1, s);
+    } else {
+      hipLaunchKernelGGL(k_vscreen, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.H,
+                         L.V, L.Vp, ub, unorm, p.mlp_wb, p.mlp_wn, p.mlp_b, summ);
+      rec(sev, 2 * t + 1, s);
+      rec(rev, 2 * t, s);
+      hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,
+                         idsl, T, t);
+      rec(rev, 2 * t + 1, s);
+    }
+  }
+}
+
+static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
+                       float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                       hipStream_t s, const aa_stream_t* lanes, int32_t n_lanes) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
-  if (B < 0 || T < 0) return AA_ERR_SHAPE;
+  if (B < 0 || T < 0 || n_lanes < 0) return AA_ERR_SHAPE;
   if (B == 0 || T == 0) return AA_OK;
-  if (!feats || !ids || !workspace) return AA_ERR_NULL;
+  if (!feats || !ids || !workspace || (n_lanes > 0 && !lanes)) return AA_ERR_NULL;
   if (!al16(feats) || !al16(workspace)) return AA_ERR_ALIGN;
   size_t need;
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
-  hipStream_t s = (hipStream_t)stream;
   const MP p = resolve(m, L);
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, s);
   if (rc) return rc;
-  const int MT = (B + 63) / 64;
-  for (int t = 0; t < T; ++t) {
-    const int cur = t & 1, nxt = cur ^ 1;
-    lstm_atten_launch(L, p, B, t ? w.keys + (size_t)(t - 1) * B : nullptr, nullptr, w.V, w.vwv, w.xg, w.h[cur],
-                      w.c[cur], w.h[nxt], w.c[nxt], w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
-                      alpha ? alpha + (size_t)t * P : nullptr, (int64_t)T * P, beta ? beta + t : nullptr, T, trace, t, s);
-    uint64_t* kt = w.keys + (size_t)t * B;
-    aa_event_t* sev = trace ? trace->screen_events : nullptr;
-    aa_event_t* rev = trace ? trace->rescore_events : nullptr;
-    rec(sev, 2 * t, s);
-    if (exact) {
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
-                         nullptr, kt);
-      rec(sev, 2 * t + 1, s);
-    } else {
-      hipLaunchKernelGGL(k_vscreen, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.H, L.V,
-                         L.Vp, w.ub, w.unorm,
-                         p.mlp_wb, p.mlp_wn, p.mlp_b, w.summ);
-      rec(sev, 2 * t + 1, s);
-      rec(rev, 2 * t, s);
-      hipLaunchKernelGGL(k_vrescore, dim3(B), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
-                         ids, T, t);
-      rec(rev, 2 * t + 1, s);
+  // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
+  int nl = n_lanes > 0 ? n_lanes : 1;
+  const int tiles = (B + 63) / 64;
+  if (nl > tiles) nl = tiles;
+  if (nl == 1) {
+    hipStream_t ls = n_lanes > 0 ? (hipStream_t)lanes[0] : s;
+    hipEvent_t e = nullptr;
+    if (ls != s) {
+      AA_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      AA_TRY(hipEventRecord(e, s));
+      AA_TRY(hipStreamWaitEvent(ls, e, 0));
     }
+    decode_rows(L, p, w, B, 0, B, T, exact, ids, alpha, beta, trace, ls);
+    if (ls != s) {
+      AA_TRY(hipEventRecord(e, ls));
+      AA_TRY(hipStreamWaitEvent(s, e, 0));
+      AA_TRY(hipEventDestroy(e));
+    }
+  } else {
+    hipEvent_t fork, join[AA_MAX_LANES];
+    if (nl > AA_MAX_LANES) nl = AA_MAX_LANES;
+    AA_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    AA_TRY(hipEventRecord(fork, s));
+    for (int i = 0; i < nl; ++i) {
+      const int r0 = (int)((int64_t)tiles * i / nl) * 64;
+      int r1 = (int)((int64_t)tiles * (i + 1) / nl) * 64;
+      if (r1 > B) r1 = B;
+      hipStream_t ls = (hipStream_t)lanes[i];
+      AA_TRY(hipStreamWaitEvent(ls, fork, 0));
+      decode_rows(L, p, w, B, r0, r1 - r0, T, exact, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
+      AA_TRY(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
+      AA_TRY(hipEventRecord(join[i], ls));
+    }
+    for (int i = 0; i < nl; ++i) {
+      AA_TRY(hipStreamWaitEvent(s, join[i], 0));
+      AA_TRY(hipEventDestroy(join[i]));
+    }
+    AA_TRY(hipEventDestroy(fork));
   }
   if (exact) {
     const int64_t n = (int64_t)B * T;
     hipLaunchKernelGGL(k_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.keys, B, T, ids);
   }
   return launch_status();
+}
+
+int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
+                     float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                     aa_stream_t stream) {
+  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
+                     nullptr, 0);
+}
+
+int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
+                           float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                           aa_stream_t stream, const aa_stream_t* lanes, int32_t n_lanes) {
+  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
+                     lanes, n_lanes);
+}
+
+// ---- decode plans: the whole greedy decode captured once into a hipGraph ------------------------
+struct aa_decode_plan {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t cap = nullptr;
+  hipStream_t lanes[AA_MAX_LANES] = {};
+  int n_lanes = 0;
+};
+
+static void plan_free(aa_decode_plan* p) {
+  if (!p) return;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  for (int i = 0; i < p->n_lanes; ++i)
+    if (p->lanes[i]) (void)hipStreamDestroy(p->lanes[i]);
+  if (p->cap) (void)hipStreamDestroy(p->cap);
+  delete p;
+}
+
+int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
+                          float* beta, void* workspace, size_t workspace_bytes, int32_t flags, int32_t n_lanes,
+                          aa_decode_plan** out) {
+  if (!out) return AA_ERR_NULL;
+  *out = nullptr;
+  Layout L;
+  int rc = check_model(m, &L);
+  if (rc) return rc;
+  if (B <= 0 || T <= 0 || n_lanes < 0 || n_lanes > AA_MAX_LANES) return AA_ERR_SHAPE;
+  if (!feats || !ids || !workspace) return AA_ERR_NULL;
+  if (!al16(feats) || !al16(workspace)) return AA_ERR_ALIGN;
+  size_t need;
+  carve_decode(nullptr, L, B, T, &need);
+  if (workspace_bytes < need) return AA_ERR_BUFFER;
+  aa_decode_plan* p = new aa_decode_plan();
+  hipError_t e = hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking);
+  const int nl = n_lanes > 1 ? n_lanes : 0;
+  for (int i = 0; e == hipSuccess && i < nl; ++i) {
+    e = hipStreamCreateWithFlags(&p->lanes[i], hipStreamNonBlocking);
+    if (e == hipSuccess) p->n_lanes = i + 1;
+  }
+  if (e == hipSuccess) e = hipStreamBeginCapture(p->cap, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    plan_free(p);
+    return (int)e;
+  }
+  rc = greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, nullptr, flags, p->cap,
+                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl);
+  e = hipStreamEndCapture(p->cap, &p->graph);
+  if (rc == 0 && e != hipSuccess) rc = (int)e;
+  if (rc == 0) {
+    e = hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) rc = (int)e;
+  }
+  if (rc) {
+    plan_free(p);
+    return rc;
+  }
+  *out = p;
+  return AA_OK;
+}
+
+int aa_decode_plan_launch(const aa_decode_plan* plan, aa_stream_t stream) {
+  if (!plan || !plan->exec) return AA_ERR_NULL;
+  return (int)hipGraphLaunch(plan->exec, (hipStream_t)stream);
+}
+
+int aa_decode_plan_destroy(aa_decode_plan* plan) {
+  plan_free(plan);
+  return AA_OK;
 }
 
 int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* scores, aa_stream_t stream) {

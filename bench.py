@@ -119,6 +119,10 @@ def main():
     ap.add_argument("--max-len", type=int, default=20)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=None, help="HIP streams the step loop is split over "
+                    "(default: the model's decode_lanes)")
+    ap.add_argument("--no-graph", action="store_true", help="launch kernels directly instead of replaying the "
+                    "captured decode plan (hipGraph)")
     ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -140,7 +144,7 @@ def main():
     ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
 
     def step(trace=None):
-        ids, alpha, beta = model.sampler(feats, max_len=T, trace=trace)
+        ids, alpha, beta = model.sampler(feats, max_len=T, trace=trace, lanes=args.lanes, graph=not args.no_graph)
         if world > 1:
             dist.all_gather_into_tensor(ids_all, ids)
         return ids
@@ -239,7 +243,9 @@ def main():
                 "weights of the reference architecture (adaptive_amd/synth.py, seed 123)",
         "config": {"workload": f"greedy decode (Encoder2Decoder.sampler) B={B}/GPU, max_len={T}",
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
-                   "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else "")},
+                   "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else ""),
+                   "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
+                   "hip_graph": not args.no_graph},
         "roofline": roofline,
         "path_roofline": {"bound": "mfma", "achieved": fl["total"] * value / 1e12, "peak": PEAK_FP32 / 1e12,
                           "unit": "TFLOP/s", "frac": fl["total"] * value / PEAK_FP32,

@@ -160,6 +160,31 @@ AA_API int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, in
                             size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                             aa_stream_t stream);
 
+/* aa_greedy_decode with the T-step loop split over up to AA_MAX_LANES streams ("lanes"): the
+ * encoder tail runs on `stream` for the whole batch, then lane i decodes its contiguous block of
+ * rows (whole 64-row tiles) on lanes[i], and `stream` waits for every lane before returning
+ * (fork/join through events, so the call is graph-capturable from `stream`).  Captions are
+ * independent, so the results equal aa_greedy_decode's bit for bit; the lanes' kernels overlap
+ * on the GPU.  trace (if any) times lane 0.  n_lanes = 0 is aa_greedy_decode. */
+#define AA_MAX_LANES 8
+AA_API int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int32_t T,
+                                  int64_t* ids, float* alpha, float* beta, void* workspace,
+                                  size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                                  aa_stream_t stream, const aa_stream_t* lanes, int32_t n_lanes);
+
+/* Decode plan: the complete greedy decode for fixed (B, T, flags, lanes) and fixed buffers,
+ * captured once into a hipGraph (one graph launch replaces the ~4T+6 kernel launches; lanes, if
+ * n_lanes > 1, are streams owned by the plan).  Launch it as often as needed on any stream; the
+ * buffers it was created with are read/written at every launch.  Results equal aa_greedy_decode's
+ * bit for bit.  The plan holds no device memory of its own besides the instantiated graph. */
+typedef struct aa_decode_plan aa_decode_plan;
+AA_API int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int32_t T,
+                                 int64_t* ids, float* alpha, float* beta, void* workspace,
+                                 size_t workspace_bytes, int32_t flags, int32_t n_lanes,
+                                 aa_decode_plan** plan);
+AA_API int aa_decode_plan_launch(const aa_decode_plan* plan, aa_stream_t stream);
+AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
+
 /* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
  * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */
 AA_API int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* scores,

@@ -15,6 +15,7 @@ for step in "$@"; do
     testsall) timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -25 gpurun_out/pytest_gpu.log ;;
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
     benchq) timeout -k 10 600 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
+    lanes) for n in 1 2 3 4; do timeout -k 10 300 python bench.py --no-cpu-baseline --no-trace --lanes $n ${LANES_ARGS:-} > gpurun_out/bench_l$n.json 2>> gpurun_out/bench.err; ok_or_fail $? lanes$n; python -c "import json;d=json.load(open('gpurun_out/bench_l$n.json'));print('lanes $n', round(d['value']), 'captions/s', round(d['ms_per_step'],3),'ms')"; done ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-trace --steps 10 > gpurun_out/prof.log 2>&1; ok_or_fail $? prof ;;
     pmc)  bash tools/pmc.sh traffic fetch write; ok_or_fail $? pmc

@@ -67,6 +67,10 @@ def test_argument_errors_without_device_work(lib):
     assert lib.aa_greedy_decode(m, None, 0, 20, None, None, None, None, 0, None, 0, None) == 0   # empty batch
     assert lib.aa_greedy_decode(m, None, 4, 20, None, None, None, None, 0, None, 0, None) == -1
     assert b"too small" in lib.aa_error_string(-4)
+    # lane-split variant: same argument checks, plus lanes
+    assert lib.aa_greedy_decode_lanes(m, None, 4, 20, None, None, None, None, 0, None, 0, None, None, -1) == -3
+    assert lib.aa_greedy_decode_lanes(m, None, 0, 20, None, None, None, None, 0, None, 0, None, None, 2) == 0
+    assert lib.aa_greedy_decode_lanes(m, 256, 4, 20, 256, None, None, 256, 10 ** 9, None, 0, None, None, 2) == -1
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):

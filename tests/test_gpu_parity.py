@@ -129,6 +129,36 @@ def test_batch_invariance(model, gpu_device):
         assert torch.equal(b2, beta[lo:hi])
 
 
+@pytest.mark.parametrize("lanes,B,exact", [(2, 512, False), (3, 300, False), (4, 200, True), (8, 100, False)])
+def test_lanes_equal_single_stream(model, gpu_device, lanes, B, exact):
+    """Splitting the step loop over HIP streams by row blocks changes nothing, bitwise."""
+    feats = torch.from_numpy(synth.make_features(B, seed=13)).to(gpu_device)
+    ref = model.sampler(feats, max_len=9, exact_vocab=exact, lanes=1)
+    got = model.sampler(feats, max_len=9, exact_vocab=exact, lanes=lanes)
+    torch.cuda.synchronize()
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+
+
+@pytest.mark.parametrize("lanes,exact", [(1, False), (2, False), (1, True), (4, True)])
+def test_graph_plan_replay_equals_direct(model, gpu_device, lanes, exact):
+    """Captured decode plans (hipGraph) give the direct path's results, also after the input buffer
+    is overwritten in place (the plan reads its buffer at every launch)."""
+    B = 192
+    feats = torch.from_numpy(synth.make_features(B, seed=17)).to(gpu_device)
+    ref = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=False)
+    for _ in range(3):  # 1st: direct, 2nd: capture + launch, 3rd: replay
+        got = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=True)
+        for r, g in zip(ref, got):
+            assert torch.equal(r, g)
+    feats.copy_(torch.from_numpy(synth.make_features(B, seed=18)).to(gpu_device))
+    ref2 = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=False)
+    got2 = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=True)
+    for r, g in zip(ref2, got2):
+        assert torch.equal(r, g)
+    assert not torch.equal(ref[0], ref2[0])
+
+
 def test_greedy_matches_oracle_odd_batch(model, oracle, gpu_device):
     B = 37
     feats = synth.make_features(B, seed=21)
