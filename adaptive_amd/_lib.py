@@ -15,8 +15,9 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 DECODE_EXACT_VOCAB = 1
+DECODE_FP32_ENCODER = 2
 MAX_LANES = 8
 
 
@@ -74,7 +75,7 @@ SIGNATURES = {
     "aa_packed_bytes": (c_size_t, [POINTER(Dims)]),
     "aa_pack_weights": (c_int, [POINTER(Model), POINTER(RefWeights), c_void_p]),
     "aa_encoder_tail": (c_int, [POINTER(Model), c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_void_p, c_void_p]),
+                                c_void_p, c_void_p, c_int32, c_void_p]),
     "aa_step_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32]),
     "aa_decode_step": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,

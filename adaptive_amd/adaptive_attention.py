@@ -202,6 +202,7 @@ class Encoder2Decoder(nn.Module):
         self._packed = None
         self._model = None
         self.decode_lanes = 1  # HIP streams the greedy step loop is split over (sampler(lanes=...))
+        self.fp32_encoder = False  # True: V GEMM on fp32 MFMA instead of the fp32-accurate bf16x3 split
         self.decode_graph = True  # replay repeated sampler calls from a captured hipGraph (aa_decode_plan)
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
@@ -282,7 +283,7 @@ class Encoder2Decoder(nn.Module):
         n = int(self.decode_lanes if lanes is None else lanes)
         if not 1 <= n <= _lib.MAX_LANES:
             raise ValueError(f"lanes must be in [1, {_lib.MAX_LANES}], got {n}")
-        flags = _lib.DECODE_EXACT_VOCAB if exact_vocab else 0
+        flags = (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
         use_graph = self.decode_graph if graph is None else bool(graph)
         if use_graph and trace is None and B > 0 and T > 0:
             # A plan binds the images pointer; it is captured the second time a key is seen, so
@@ -351,7 +352,8 @@ class Encoder2Decoder(nn.Module):
         VWv = torch.empty(B, ATT, 64, device=dev)
         with torch.cuda.device(dev):
             rc = lib.aa_encoder_tail(model, images.data_ptr(), B, a_g.data_ptr(), V.data_ptr(), v_g.data_ptr(),
-                                     h0.data_ptr(), c0.data_ptr(), VWv.data_ptr(), _lib.stream_handle())
+                                     h0.data_ptr(), c0.data_ptr(), VWv.data_ptr(),
+                                     _lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0, _lib.stream_handle())
         _lib.check(rc, "encoder_tail")
         return V, v_g, (h0, c0), a_g, VWv
 

@@ -63,7 +63,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, wgs;
+  size_t enc_a_w, enc_a_b, enc_w3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, wgs;
   size_t total_floats;
 };
 
@@ -80,6 +80,7 @@ static Layout make_layout(const aa_dims& d) {
   auto take = [&](size_t n) { size_t r = o; o = al64(o + n); return r; };
   L.enc_a_w = take((size_t)L.H * L.C);
   L.enc_a_b = take(L.H);
+  L.enc_w3 = take((size_t)3 * L.H * L.C / 2);  // bf16 [H/32][C/16][3][64][8]
   L.heads_w = take((size_t)L.NHp * L.C);
   L.heads_b = take(L.NHp);
   L.wv = take((size_t)PP * L.H);
@@ -101,6 +102,7 @@ static Layout make_layout(const aa_dims& d) {
 }
 
 struct MP {  // resolved device pointers of the packed weights
+  const bf16x8* enc_w3;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const uint16_t* mlp_wb;
@@ -110,6 +112,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   const float* b = static_cast<const float*>(m->packed);
   MP p;
   p.enc_a_w = b + L.enc_a_w; p.enc_a_b = b + L.enc_a_b;
+  p.enc_w3 = reinterpret_cast<const bf16x8*>(b + L.enc_w3);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -230,6 +233,167 @@ __global__ __launch_bounds__(256) void k_enc_v(const float* __restrict__ feats, 
   for (int r = 0; r < 16; ++r) {
     const int row = mt * BM + wm * 32 + acc_row(r, lane);
     if (row < M) V[(int64_t)row * H + col] = reluf_(acc[0][0][r] + bv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// E1 (default): the same V on bf16 MFMA with 3-way split operands ("bf16x3"), fp32-accurate.
+// Every fp32 operand x is split exactly as x = x0 + x1 + x2 + r with x_i bf16 (x0 = bf16(x),
+// x1 = bf16(x - x0), x2 = bf16(x - x0 - x1); each difference is exact in fp32, |r| <= 2^-24 |x|).
+// a.w is accumulated from the six partial products with i + j <= 2 (smallest first); the three
+// dropped ones are <= 2^-24 |a w| each, so the result is as accurate as an fp32 GEMM (whose own
+// accumulation error over K = 2048 dominates), at 6 bf16 MFMAs (6 x 32 cycles) per 32x32x16
+// block instead of 8 fp32 MFMAs (8 x 64 cycles).
+//   W: pre-split at pack time into MFMA-fragment order, enc_w3[nb][kc][q][lane][8] (1 KB per
+//      fragment: lane l holds W[32 nb + (l & 31)][16 kc + 8 (l >> 5) + j]) and read straight into
+//      VGPRs one stage ahead (each fragment is one coalesced 16-B-per-lane load).
+//   A: read from the NCHW feature map (row m = b*49 + p, column = channel; lanes over consecutive
+//      rows -> contiguous addresses), split in registers, staged in LDS as three bf16 planes
+//      [row][k] with an 80-B pitch (conflict-free ds_read_b128 / ds_write_b128).
+// Tile 128 x 128 per 256-thread workgroup; each wave owns 64 x 64 (2 x 2 blocks of 32 x 32);
+// K in stages of 32 (two k16 MFMA steps), A double-buffered in LDS, A and W prefetched a stage
+// ahead in registers.
+// ---------------------------------------------------------------------------------------------
+constexpr int EV_BM = 128, EV_BN = 128, EV_BK = 32, EV_LD = 40;  // LDS pitch in bf16 (80 B)
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  const float r2 = r1 - (float)m;
+  l = (__bf16)r2;
+}
+
+__global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ feats, int B, int C, int H,
+                                                   const bf16x8* __restrict__ W3, const float* __restrict__ bias,
+                                                   float* __restrict__ V) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][EV_BM * EV_LD];
+  const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN, KC = C / 16;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int mt = L / NTn, nt = L % NTn;  // n fastest: the A tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  // A staging: thread -> row r (0..127), k-half kh: k = 16 kh + i, i < 16, of each 32-stage
+  const int r = t & (EV_BM - 1), kh = t >> 7;
+  int m = mt * EV_BM + r;
+  m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
+  const int bi = m / P, pi = m - bi * P;
+  const float* arow = feats + (int64_t)bi * C * P + pi + (int64_t)(16 * kh) * P;
+  // W fragments of this wave: n-blocks nb0 + c (c = 0, 1)
+  const int nb0 = (nt * EV_BN + wn * 64) / 32;
+  const bf16x8* wf0 = W3 + (size_t)nb0 * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  float ra[16];
+  bf16x8 wa[2][2][3], wb[2][2][3];  // [sub][c][q], two stages in flight
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.f;
+
+  auto gload_a = [&](int s) {
+    const float* src = arow + (int64_t)(EV_BK * s) * P;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ra[i] = src[i * P];
+  };
+  auto gload_w = [&](int s, bf16x8 (&w)[2][2][3]) {
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const size_t o = ((size_t)(2 * s + sub) * 3 + q) * 64;
+        w[sub][0][q] = wf0[o];
+        w[sub][1][q] = wf1[o];
+      }
+  };
+  auto lstore_a = [&](int buf) {
+    bf16x8 h[2], md[2], lo[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __bf16 x0, x1, x2;
+      split3(ra[i], x0, x1, x2);
+      h[i >> 3][i & 7] = x0;
+      md[i >> 3][i & 7] = x1;
+      lo[i >> 3][i & 7] = x2;
+    }
+    const int o = r * EV_LD + 16 * kh;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      *reinterpret_cast<bf16x8*>(&As[buf][0][o + 8 * j]) = h[j];
+      *reinterpret_cast<bf16x8*>(&As[buf][1][o + 8 * j]) = md[j];
+      *reinterpret_cast<bf16x8*>(&As[buf][2][o + 8 * j]) = lo[j];
+    }
+  };
+  auto compute = [&](int buf, const bf16x8 (&w)[2][2][3]) {
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      bf16x8 fa[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          fa[a][q] = *reinterpret_cast<const bf16x8*>(&As[buf][q][(wm * 64 + a * 32 + li) * EV_LD + 16 * sub + 8 * lh]);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          floatx16 x = acc[a][c];
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], w[sub][c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], w[sub][c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][2], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], w[sub][c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][0], x, 0, 0, 0);
+          acc[a][c] = x;
+        }
+    }
+  };
+
+  const int ns = C / EV_BK;  // even (C % 64 == 0 checked by the host)
+  gload_a(0);
+  gload_w(0, wa);
+  lstore_a(0);
+  gload_a(1);
+  gload_w(1, wb);
+  __syncthreads();
+  // No branches around the prefetch loads (a branch makes the compiler's vmcnt bookkeeping assume
+  // the worst at the join and drain the A prefetch inside the MFMA stream): past the end the
+  // stage index is clamped and the extra loads / LDS stores are harmless.
+  for (int s = 0; s < ns; s += 2) {
+    const int s2 = s + 2 < ns ? s + 2 : ns - 1, s3 = s + 3 < ns ? s + 3 : ns - 1;
+    // stage s: A in As[0], W in wa; A of s+1 in ra, W of s+1 in wb
+    // (sched_barrier: keep the scheduler from hoisting the split of a just-issued A prefetch into
+    //  the MFMA stream above it, which would wait for the load right away)
+    lstore_a(1);
+    gload_a(s2);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0, wa);
+    gload_w(s2, wa);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    // stage s+1: A in As[1], W in wb (As[0] is free: its last reader passed the barrier)
+    lstore_a(0);
+    gload_a(s3);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1, wb);
+    gload_w(s3, wb);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int colb = nt * EV_BN + wn * 64 + li;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = colb + 32 * c;
+    const float bv = bias[col];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = mt * EV_BM + wm * 64 + a * 32 + acc_row(i, lane);
+        if (row < M) V[(int64_t)row * H + col] = reluf_(acc[a][c][i] + bv);
+      }
   }
 }
 
@@ -885,6 +1049,24 @@ __global__ void k_pack_lstm(const float* __restrict__ w_ih, const float* __restr
 }
 
 // wgs[tile][j][u] = (j < 49 ? W_g[j] : W_s[j - 49])[tile*16 + u]
+// W_a split into three bf16 planes in MFMA-fragment order (see k_enc_v3): block = (nb, kc), lane l
+// -> W[32 nb + (l & 31)][16 kc + 8 (l >> 5) + j], planes q = 0, 1, 2 at out[((nb KC + kc) 3 + q) 64 + l].
+__global__ void k_pack_w3(const float* __restrict__ w, int C, bf16x8* __restrict__ out) {
+  const int KC = C / 16, nb = blockIdx.x / KC, kc = blockIdx.x % KC, l = threadIdx.x;
+  const float* src = w + (int64_t)(32 * nb + (l & 31)) * C + 16 * kc + 8 * (l >> 5);
+  bf16x8 h, m, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 a, b, c;
+    split3(src[j], a, b, c);
+    h[j] = a; m[j] = b; lo[j] = c;
+  }
+  bf16x8* o = out + ((size_t)blockIdx.x * 3) * 64 + l;
+  o[0] = h;
+  o[64] = m;
+  o[128] = lo;
+}
+
 __global__ void k_pack_wgs(const float* __restrict__ wg, const float* __restrict__ ws, int H, float* __restrict__ out) {
   const int tile = blockIdx.x;
   for (int i = threadIdx.x; i < 2 * P * 16; i += blockDim.x) {
@@ -953,7 +1135,7 @@ const char* aa_error_string(int code) {
   switch (code) {
     case AA_OK: return "ok";
     case AA_ERR_NULL: return "a required pointer is NULL";
-    case AA_ERR_DIMS: return "unsupported model dimensions (need embed%32==0, hidden%256==0, hidden<=1024, vocab>=1, channels%32==0, spatial==49)";
+    case AA_ERR_DIMS: return "unsupported model dimensions (need embed%32==0, hidden%256==0, hidden<=1024, vocab>=1, channels%64==0, spatial==49)";
     case AA_ERR_SHAPE: return "bad batch size or step count";
     case AA_ERR_BUFFER: return "packed-weight or workspace buffer too small";
     case AA_ERR_ALIGN: return "a device pointer is not 16-byte aligned";
@@ -964,7 +1146,7 @@ const char* aa_error_string(int code) {
 int aa_check_dims(const aa_dims* d) {
   if (!d) return AA_ERR_NULL;
   if (d->embed <= 0 || d->embed % 32 || d->hidden <= 0 || d->hidden % 256 || d->hidden > MAX_H || d->vocab < 1 ||
-      d->channels <= 0 || d->channels % 32 || d->spatial != P)
+      d->channels <= 0 || d->channels % 64 || d->spatial != P)
     return AA_ERR_DIMS;
   return AA_OK;
 }
@@ -1025,6 +1207,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H,
                      reinterpret_cast<uint16_t*>(base + L.mlp_wb), base + L.mlp_wn);
   hipLaunchKernelGGL(k_pack_wgs, dim3(H / 16), dim3(256), 0, s, w->att_affine_g_w, w->att_affine_s_w, H, base + L.wgs);
+  hipLaunchKernelGGL(k_pack_w3, dim3((H / 32) * (C / 16)), dim3(64), 0, s, w->enc_affine_a_w, C,
+                     reinterpret_cast<bf16x8*>(base + L.enc_w3));
   return launch_status();
 }
 
@@ -1033,16 +1217,20 @@ static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
 }
 
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
-                          float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, hipStream_t s) {
+                          float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
+                          hipStream_t s) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
   rec(ev, 0, s);
   hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, feats, nch, a_g);
   rec(ev, 1, s);
   rec(ev, 2, s);
-  {
+  if (flags & AA_DECODE_FP32_ENCODER) {
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
+  } else {
+    const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN;
+    hipLaunchKernelGGL(k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_w3, p.enc_a_b, V);
   }
   rec(ev, 3, s);
   rec(ev, 4, s);
@@ -1062,7 +1250,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
 }
 
 int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g, float* V, float* v_g, float* h0,
-                    float* c0, float* VWv, aa_stream_t stream) {
+                    float* c0, float* VWv, int32_t flags, aa_stream_t stream) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
@@ -1070,7 +1258,8 @@ int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g
   if (B == 0) return AA_OK;
   if (!feats || !a_g || !V || !v_g || !h0 || !c0) return AA_ERR_NULL;
   if (!al16(feats) || !al16(a_g) || !al16(V) || !al16(VWv) || !al16(v_g)) return AA_ERR_ALIGN;
-  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, nullptr, nullptr, (hipStream_t)stream);
+  return encoder_launch(L, resolve(m, L), feats, B, a_g, V, v_g, h0, c0, VWv, nullptr, nullptr, flags,
+                        (hipStream_t)stream);
 }
 
 // ---- workspace carving ----------------------------------------------------------------------
@@ -1265,7 +1454,7 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
-                      trace ? trace->encoder_events : nullptr, s);
+                      trace ? trace->encoder_events : nullptr, flags, s);
   if (rc) return rc;
   // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
   int nl = n_lanes > 0 ? n_lanes : 1;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 3
+#define AA_ABI_VERSION 4
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -122,9 +122,11 @@ AA_API int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream
  * h0/c0 = tanh(a_g W^T + b); plus the step-invariant VWv = V W_v^T used by every decode step.
  * Replaces AttentiveCNN.forward after resnet_conv (baseline_attention.py:46-62).
  * feats: [B, C, 7, 7] NCHW post-trunk features.  Outputs: a_g [B,C], V [B,P,H], v_g [B,E],
- * h0 [B,H], c0 [B,H], VWv [B,P,64] (columns >= P are zero; may be NULL). */
+ * h0 [B,H], c0 [B,H], VWv [B,P,64] (columns >= P are zero; may be NULL).  flags: 0 or
+ * AA_DECODE_FP32_ENCODER. */
 AA_API int aa_encoder_tail(const aa_model* m, const float* feats, int32_t B, float* a_g, float* V,
-                           float* v_g, float* h0, float* c0, float* VWv, aa_stream_t stream);
+                           float* v_g, float* h0, float* c0, float* VWv, int32_t flags,
+                           aa_stream_t stream);
 
 /* Workspace for aa_decode_step at batch B. */
 AA_API size_t aa_step_workspace_bytes(const aa_dims* dims, int32_t B);
@@ -146,6 +148,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 /* Decode flags */
 #define AA_DECODE_EXACT_VOCAB 1 /* compute every fp32 logit (fp32 MFMA GEMM + fused argmax) instead of
                                    the bf16 screen + exact fp32 rescoring; both give the same ids */
+#define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of
+                                    the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v3) */
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];

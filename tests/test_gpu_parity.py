@@ -66,6 +66,31 @@ def test_encoder_tail(model, oracle, gpu_device):
     assert np.all(got[..., 49:] == 0)
 
 
+def test_split_bf16_encoder_is_fp32_accurate(model, oracle, gpu_device):
+    """k_enc_v3 (3-way bf16 split on bf16 MFMA) vs an fp64 reference: its error is of the same order
+    as the fp32-MFMA encoder's (K = 2048 fp32 accumulation), far below the 2e-5 parity tolerance.
+    B = 67 -> 3283 rows: a ragged last 128-row tile."""
+    B = 67
+    feats = torch.from_numpy(synth.make_features(B, seed=3)).to(gpu_device)
+    V3 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
+    model.fp32_encoder = True
+    try:
+        V1 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
+    finally:
+        model.fp32_encoder = False
+    A = feats.cpu().numpy().astype(np.float64).reshape(B, 2048, 49).transpose(0, 2, 1)
+    W = oracle.w["encoder.affine_a.weight"].numpy().astype(np.float64)
+    b = oracle.w["encoder.affine_a.bias"].numpy().astype(np.float64)
+    pre = A @ W.T + b
+    ref = np.maximum(pre, 0.0)
+    scale = np.abs(A) @ np.abs(W).T + np.abs(b)          # sum_k |a_k w_k| + |b| per output
+    e3 = np.abs(V3 - ref) / scale
+    e1 = np.abs(V1 - ref) / scale
+    assert e3.max() < 2e-6, e3.max()                     # fp32 GEMM class: ~K u / sqrt(K) << 1e-5
+    assert e3.max() < 4 * e1.max() + 1e-7, (e3.max(), e1.max())
+    assert np.abs(V3 - ref).max() < ATT_TOL / 2
+
+
 def test_decode_step_logits(model, oracle, gpu_device):
     """One Decoder.forward step (T == 1) from the encoder states: logits within 1e-4."""
     B = 7
