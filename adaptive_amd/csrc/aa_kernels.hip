@@ -44,11 +44,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // both fp32 accumulations add <= gamma_H * sum|uw| each (gamma_512 ~ 3.1e-5).  Hence
 // |A - L| <= (0.0078125 + 1.6e-5 + 6.2e-5 (+ bias roundings)) * sum_k |u_k w_k|
 //         <= 0.00791 * ||u||_2 ||w||_2   (Cauchy-Schwarz).
-// CEPS = 0.0085 adds ~7% slack (norms are themselves fp32 and inflated by 1e-5); EPS_REL covers
-// the bias additions.  A column n is a candidate iff A_n + eps_n >= max_m (A_m - eps_m): every
-// column holding the exact-fp32 maximum passes, every rejected column is strictly below it.
+// The screen applies one bound per (row, 32-column granule g):
+//   E = CEPS ||u|| W_g + EPS_ABS (||u|| W_g + B_g),   W_g = max_{n in g} ||w_n||, B_g = max |b_n|
+// CEPS = 0.0085 adds ~7% slack (norms are fp32 and inflated by 1e-5); the EPS_ABS term bounds
+// 2^-17 |A| >= the bias-addition roundings plus the < 32-ulp truncation of the screened values
+// that carries the arg-max in their low bits (|A| <= ||u|| ||w_n|| (1 + 2^-7) + |b_n|).  A column
+// n is a candidate iff A_n + E >= max_m (A_m - E): every column holding the exact-fp32 maximum
+// passes, every rejected column is strictly below it.
 constexpr float CEPS = 0.0085f;
-constexpr float EPS_REL = 1e-6f;
+constexpr float EPS_ABS = 1e-5f;
 constexpr int VS_TILE = 32;     // screen summary granule: one (lbmax, top-2 ub) per row per 32 columns
 constexpr int RS_CAP = 2048;    // candidate list capacity per row in k_vrescore (else full row)
 // Exact fp32 logits (k_vocab and the rescoring) are NP_VOCAB independent fma chains over contiguous
@@ -63,7 +67,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, wgs;
+  size_t enc_a_w, enc_a_b, enc_w3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs;
   size_t total_floats;
 };
 
@@ -96,6 +100,7 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_b = take(L.Vp);
   L.mlp_wb = take((size_t)L.Vp * L.H / 2);  // bf16
   L.mlp_wn = take(L.Vp);
+  L.mlp_gs = take((size_t)2 * (L.Vp / VS_TILE));  // float2 per granule: (max ||w_n||, max |b_n|)
   L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
   L.total_floats = o;
   return L;
@@ -105,6 +110,7 @@ struct MP {  // resolved device pointers of the packed weights
   const bf16x8* enc_w3;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
+  const float2* mlp_gs;
   const uint16_t* mlp_wb;
 };
 
@@ -118,6 +124,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
   p.mlp_w = b + L.mlp_w; p.mlp_b = b + L.mlp_b;
   p.mlp_wb = reinterpret_cast<const uint16_t*>(b + L.mlp_wb); p.mlp_wn = b + L.mlp_wn; p.wgs = b + L.wgs;
+  p.mlp_gs = reinterpret_cast<const float2*>(b + L.mlp_gs);
   return p;
 }
 
@@ -144,6 +151,14 @@ __device__ __forceinline__ uint64_t argmax_key(float x, int n) {
   uint32_t u = __float_as_uint(x);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   return ((uint64_t)u << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)n);
+}
+// order-preserving map of a (finite) float to u32: a < b  <=>  order_key(a) < order_key(b)
+__device__ __forceinline__ uint32_t order_key(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 __device__ __forceinline__ int64_t key_token(uint64_t k) { return (int64_t)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFu)); }
 
@@ -710,32 +725,38 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __re
 }
 
 // ---------------------------------------------------------------------------------------------
-// D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a 64x64
-// tile (4 waves 2x2, v_mfma_f32_32x32x16_bf16, operands straight from L2), then per (row, tile):
-//   lbmax = max_n (A_n - eps_n),  (ub1, idx1) = top of A_n + eps_n,  ub2 = second largest upper bound
-// with eps_n = CEPS ||u|| ||w_n|| + EPS_REL |A_n| (see CEPS).  Summary -> summ[row][tile] (16 B).
+// D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a
+// 128x128 tile, then per (row, 32-column granule g) with the granule's bound E (see CEPS):
+//   summ[row][g] = {max_n A_n - E, max_n A_n + E, second largest A_n + E, arg-max column}.
 // ---------------------------------------------------------------------------------------------
-struct Top2 {
-  float lb, ub1, ub2;
-  int idx;
-};
-__device__ __forceinline__ Top2 top2_merge(Top2 a, Top2 b) {
-  Top2 r;
-  r.lb = fmaxf(a.lb, b.lb);
-  if (a.ub1 > b.ub1 || (a.ub1 == b.ub1 && a.idx <= b.idx)) {
-    r.ub1 = a.ub1; r.idx = a.idx; r.ub2 = fmaxf(a.ub2, b.ub1);
-  } else {
-    r.ub1 = b.ub1; r.idx = b.idx; r.ub2 = fmaxf(b.ub2, a.ub1);
-  }
-  return r;
+// Partner exchange for the screen epilogue's butterfly over the 32 lanes of a column block: level
+// M pairs each lane with one whose index differs in bit M and agrees in the bits above it --
+// M = 16: ds_swizzle xor 16; 8: DPP row_mirror (i <-> 15 - i); 4: row_half_mirror (i <-> 7 - i);
+// 2, 1: DPP quad_perm xor 2 / xor 1.  No LDS traffic except the one swizzle level.
+template <int M>
+__device__ __forceinline__ uint32_t partner(uint32_t v) {
+  if constexpr (M == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+  else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+  else if constexpr (M == 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
 }
-__device__ __forceinline__ Top2 shfl_xor_top2(Top2 a, int o) {
-  Top2 r;
-  r.lb = __shfl_xor(a.lb, o, 64);
-  r.ub1 = __shfl_xor(a.ub1, o, 64);
-  r.ub2 = __shfl_xor(a.ub2, o, 64);
-  r.idx = __shfl_xor(a.idx, o, 64);
-  return r;
+
+// One transposing butterfly step: a lane carrying M rows keeps half of them (the upper half if
+// bit M of its lane index is set) merged with its partner's copy of the same rows.  Merge: top-2
+// of the keys.
+template <int M>
+__device__ __forceinline__ void screen_bfly(uint32_t (&k1)[16], uint32_t (&k2)[16], int li) {
+  const bool hi = (li & M) != 0;
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    const uint32_t s1 = hi ? k1[k] : k1[k + M / 2], s2 = hi ? k2[k] : k2[k + M / 2];
+    const uint32_t m1 = hi ? k1[k + M / 2] : k1[k], m2 = hi ? k2[k + M / 2] : k2[k];
+    const uint32_t r1 = partner<M>(s1), r2 = partner<M>(s2);
+    k1[k] = m1 > r1 ? m1 : r1;
+    const uint32_t lo = m1 > r1 ? r1 : m1, h2 = m2 > r2 ? m2 : r2;
+    k2[k] = lo > h2 ? lo : h2;
+  }
 }
 
 // Screen tile: 128 rows x 128 columns per workgroup, K in 64-wide bf16 steps staged through
@@ -744,7 +765,7 @@ __device__ __forceinline__ Top2 shfl_xor_top2(Top2 a, int o) {
 constexpr int SC_BM = 128, SC_BN = 128, SC_BK = 64, SC_LD = SC_BK + 8;  // LDS row pitch in bf16
 __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp, const uint16_t* __restrict__ ub,
                                                     const float* __restrict__ unorm, const uint16_t* __restrict__ wb,
-                                                    const float* __restrict__ wn, const float* __restrict__ bias,
+                                                    const float2* __restrict__ gs, const float* __restrict__ bias,
                                                     float4* __restrict__ summ) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (SC_BM + SC_BN) * SC_LD];
   __shared__ float un_s[SC_BM];
@@ -815,39 +836,50 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp,
   }
 #undef SC_GLOAD
 #undef SC_LSTORE
-  // epilogue: per wave, each 32-row block's (lb, ub) -> a private LDS slab; 2 lanes per row each
-  // summarise one 32-column granule (lbmax, top-2 ub) -> summ[row][col / 32].
-  float2* slab = reinterpret_cast<float2*>(lds) + wave * 32 * 65;  // [32][65] per wave
+  // epilogue: screened logits A = acc + b -> order-preserving u32 keys whose low 5 bits are replaced
+  // by the column's position in its granule (truncation < 32 ulp, covered by EPS_ABS), then per
+  // (row, 32-column granule) a transposing butterfly over the 32 lanes that hold the granule's
+  // columns (levels 16, 8, 4, 2 each halve the rows a lane carries; level 1 completes): k1 = max
+  // key (value and arg-max), k2 = second largest.  The bound E of the granule is applied last.
+  const int G0 = (n0 + wn_ * 64) / VS_TILE;
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
+  for (int c = 0; c < 2; ++c) {
+    const int col = n0 + wn_ * 64 + c * 32 + li;
+    const bool valid = col < V;
+    const float bv = bias[col];
+    const float2 gsv = gs[G0 + c];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int col = n0 + wn_ * 64 + c * 32 + li;
-      const bool valid = col < V;
-      const float bv = bias[col], wnv = wn[col];
+    for (int a = 0; a < 2; ++a) {
+      uint32_t k1[16], k2[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int rl = acc_row(r, lane);
-        const float x = acc[a][c][r] + bv;
-        const float eps = CEPS * un_s[wm * 64 + a * 32 + rl] * wnv + EPS_REL * fabsf(x);
-        slab[rl * 65 + c * 32 + li] = valid ? make_float2(x - eps, x + eps) : make_float2(-INFINITY, -INFINITY);
+        const uint32_t key = order_key(acc[a][c][r] + bv);
+        k1[r] = valid ? (key & ~31u) | (uint32_t)li : 0u;
+        k2[r] = 0u;
+      }
+      screen_bfly<16>(k1, k2, li);
+      screen_bfly<8>(k1, k2, li);
+      screen_bfly<4>(k1, k2, li);
+      screen_bfly<2>(k1, k2, li);
+      const uint32_t r1 = partner<1>(k1[0]), r2 = partner<1>(k2[0]);
+      const uint32_t m1 = k1[0] > r1 ? k1[0] : r1;
+      const uint32_t lo = k1[0] > r1 ? r1 : k1[0], h2 = k2[0] > r2 ? k2[0] : r2;
+      const uint32_t m2 = lo > h2 ? lo : h2;
+      const int rr = (li >> 1) & 15;  // this lane pair now holds row acc_row(rr) of the block
+      const int rl = wm * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      const int row = m0 + rl;
+      if (!(li & 1) && row < B) {
+        float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        if (m1) {
+          const float un = un_s[rl], uw = un * gsv.x;
+          const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+          const float x1 = key_value(m1 & ~31u);
+          const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
+          o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + c) * VS_TILE + (int)(m1 & 31u)));
+        }
+        summ[(int64_t)row * NTn + G0 + c] = o;
       }
     }
-    __syncthreads();
-    {
-      const int rl = lane >> 1, hq = lane & 1;
-      Top2 x{-INFINITY, -INFINITY, -INFINITY, 0};
-      const int cbase = n0 + wn_ * 64 + hq * 32;
-      for (int cc = 0; cc < 32; ++cc) {
-        const float2 v = slab[rl * 65 + hq * 32 + cc];
-        x.lb = fmaxf(x.lb, v.x);
-        if (v.y > x.ub1) { x.ub2 = x.ub1; x.ub1 = v.y; x.idx = cbase + cc; }
-        else x.ub2 = fmaxf(x.ub2, v.y);
-      }
-      const int row = m0 + wm * 64 + a * 32 + rl;
-      if (row < B) summ[(int64_t)row * NTn + cbase / VS_TILE] = make_float4(x.lb, x.ub1, x.ub2, __int_as_float(x.idx));
-    }
-    __syncthreads();
   }
 }
 
@@ -1089,6 +1121,14 @@ __global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, uint16_t* 
   if (lane == 0) wn[n] = sqrtf(s) * 1.00001f;
 }
 
+// Per 32-column granule of the vocab: (max_n ||w_n||, max_n |b_n|) for the screen's bound.
+__global__ void k_pack_gs(const float* __restrict__ wn, const float* __restrict__ b, float2* __restrict__ gs) {
+  const int g = blockIdx.x, l = threadIdx.x;  // 64 threads, lanes >= 32 mirror 0..31
+  const int n = g * VS_TILE + (l & (VS_TILE - 1));
+  const float mw = wave_max(wn[n]), mb = wave_max(fabsf(b[n]));
+  if (l == 0) gs[g] = make_float2(mw, mb);
+}
+
 __device__ __forceinline__ uint64_t splitmix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -1206,6 +1246,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   gemm_bias(w->embed_w, E, V, base + L.wemb, E, L.N5, E, nullptr, base + L.table, L.N5, s);
   hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H,
                      reinterpret_cast<uint16_t*>(base + L.mlp_wb), base + L.mlp_wn);
+  hipLaunchKernelGGL(k_pack_gs, dim3(L.Vp / VS_TILE), dim3(64), 0, s, base + L.mlp_wn, base + L.mlp_b,
+                     reinterpret_cast<float2*>(base + L.mlp_gs));
   hipLaunchKernelGGL(k_pack_wgs, dim3(H / 16), dim3(256), 0, s, w->att_affine_g_w, w->att_affine_s_w, H, base + L.wgs);
   hipLaunchKernelGGL(k_pack_w3, dim3((H / 32) * (C / 16)), dim3(64), 0, s, w->enc_affine_a_w, C,
                      reinterpret_cast<bf16x8*>(base + L.enc_w3));
@@ -1427,7 +1469,7 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
       rec(sev, 2 * t + 1, s);
     } else {
       hipLaunchKernelGGL(k_vscreen, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.H,
-                         L.V, L.Vp, ub, unorm, p.mlp_wb, p.mlp_wn, p.mlp_b, summ);
+                         L.V, L.Vp, ub, unorm, p.mlp_wb, p.mlp_gs, p.mlp_b, summ);
       rec(sev, 2 * t + 1, s);
       rec(rev, 2 * t, s);
       hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,

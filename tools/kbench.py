@@ -1,0 +1,44 @@
+"""Drive tools/kbench.hip: time individual product kernels (and variants) on a real workspace.
+usage (GPU box): python tools/kbench.py [kernel ...]"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from adaptive_amd import Config, Encoder2Decoder, _lib  # noqa: E402
+from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
+
+SO = os.path.join(ROOT, "tools", "_build", "libkbench.so")
+
+
+def main():
+    names = sys.argv[1:] or ["lstm", "atten", "vscreen", "vrescore", "enc_v3"]
+    if not os.path.exists(SO):
+        os.makedirs(os.path.dirname(SO), exist_ok=True)
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+                               "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include"),
+                               os.path.join(ROOT, "tools", "kbench.hip"), "-o", SO])
+    dev = torch.device("cuda", 0)
+    model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    B, T = 512, 20
+    feats = synthetic_features(B, dev, seed=0)
+    model.sampler(feats, max_len=T, graph=False)
+    torch.cuda.synchronize()
+    lib = ctypes.CDLL(SO)
+    lib.kb_time.restype = ctypes.c_int
+    lib.kb_time.argtypes = [ctypes.POINTER(_lib.Model), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                            ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+    m = model._model_struct()
+    for n in names:
+        out = ctypes.c_float()
+        reps = 20 if n.startswith("enc") else 200
+        rc = lib.kb_time(m, feats.data_ptr(), model._ws.data_ptr(), B, T, n.encode(), reps, ctypes.byref(out))
+        print(f"{n:24s} rc={rc} {out.value:9.2f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
