@@ -67,7 +67,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs;
+  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs;
   size_t total_floats;
 };
 
@@ -92,6 +92,7 @@ static Layout make_layout(const aa_dims& d) {
   L.ws = take((size_t)P * L.H);
   L.wh = take(PP);
   L.whh = take((size_t)4 * L.H * L.H);
+  L.whh3 = take((size_t)3 * 4 * L.H * L.H / 2);  // bf16 fragments [4H/32][H/16][3][64][8]
   L.wemb = take((size_t)L.N5 * L.E);
   L.wvg = take((size_t)L.N5 * L.E);
   L.bias5 = take(L.N5);
@@ -107,7 +108,7 @@ static Layout make_layout(const aa_dims& d) {
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const bf16x8* enc_w3;
+  const bf16x8 *enc_w3, *whh3;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const float2* mlp_gs;
@@ -119,6 +120,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   MP p;
   p.enc_a_w = b + L.enc_a_w; p.enc_a_b = b + L.enc_a_b;
   p.enc_w3 = reinterpret_cast<const bf16x8*>(b + L.enc_w3);
+  p.whh3 = reinterpret_cast<const bf16x8*>(b + L.whh3);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -484,114 +486,251 @@ __global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, 
 // ---------------------------------------------------------------------------------------------
 constexpr int PART = 128;  // partial-projection row pitch (2 x 49 used)
 
-// 512 threads: two groups of 4 waves run the two halves of K (each its own double-buffered LDS),
-// group 1's accumulators are added to group 0's in a fixed order (g0 + g1), then the epilogue.
-__global__ __launch_bounds__(512) void k_lstm(int B, int H, int V, const uint64_t* __restrict__ keys_prev,
-                                              const int64_t* __restrict__ tok_in, const float* __restrict__ table,
-                                              const float* __restrict__ xg, const float* __restrict__ h_in,
-                                              const float* __restrict__ c_in, const float* __restrict__ whh,
+// The GEMM h_{t-1} W_hh^T runs on bf16 MFMA with 3-way split operands (see k_enc_v3): h arrives
+// already split (hsp_in, written by the previous step's epilogue or k_split_rows) and W_hh is
+// pre-split at pack time, both in MFMA-fragment order, so every operand is one coalesced 16-B
+// load per lane straight into VGPRs -- no LDS staging.  Fragment index of (row block rb, k16
+// chunk kc, plane q): ((rb * KC + kc) * 3 + q) * 64 + lane.
+// 512 threads = 8 waves; wave w computes the whole 64x64 tile (2 x 2 blocks of 32x32) over K
+// chunks [w KC/8, (w+1) KC/8), so no fragment is loaded twice in the workgroup; the eight partial
+// tiles meet in LDS and are summed in a fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)).
+__device__ __forceinline__ void x3_step(floatx16& acc, const bf16x8 (&a)[3], const bf16x8 (&w)[3]) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], acc, 0, 0, 0);
+}
+
+constexpr int LS_CP = 68;  // k_lstm LDS tile pitch (floats): conflict-free cell reads
+
+template <int H>
+__global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+                                              const float* __restrict__ table,
+                                              const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
+                                              const float* __restrict__ c_in, const bf16x8* __restrict__ whh3,
                                               const float* __restrict__ wgs, float* __restrict__ h_out,
-                                              float* __restrict__ c_out, float* __restrict__ s_out,
-                                              float* __restrict__ part) {
-  constexpr int BM = 64, BN = 64;
-  __shared__ __attribute__((aligned(16))) float lds[2 * Tile<BM, BN>::LDS_FLOATS];
-  const int MT = (B + BM - 1) / BM, NTn = H / 16;
+                                              bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                              float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
+  constexpr int WSP = 100;  // 98 projection outputs padded to whole float4s
+  __shared__ __attribute__((aligned(16))) float lds[8 * TS + 2 * 64 * 16 + 16 * WSP];
+  constexpr int NTn = H / 16, KC = H / 16;
+  const int MT = (B + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
-  const int t = threadIdx.x, grp = t >> 8, tg = t & 255;
-  const int lane = t & 63, wave = tg >> 6, wm = wave >> 1, wn = wave & 1;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m0 = mt * BM;
-  const int nkh = H / BK / 2;
-  ARowMajor al{h_in, H, m0, B};
-  WRowMajor wl{whh, H, nt * BN};
-  floatx16 acc[1][1];
-  gemm_mainloop<BM, BN>(al, wl, nkh, lds + grp * Tile<BM, BN>::LDS_FLOATS, acc, tg, grp * nkh);
-  constexpr int CP = 68;
-  float* Cs = lds;                 // [64][CP] gate pre-activations
-  float* C1 = Cs + 64 * CP;        // [64][CP] group-1 partial sums
-  float* Hs = C1 + 64 * CP;        // [64][16] h' of the tile
+  float* Pt = lds;                 // [8][64][CP] partial tiles; slot 0 becomes the summed tile
+  float* Hs = Pt + 8 * TS;         // [64][16] h' of the tile
   float* Ss = Hs + 64 * 16;        // [64][16] s of the tile
-  float* Wsl = Ss + 64 * 16;       // [98][17] W_g / W_s columns of the tile's units (padded)
-  if (grp == 1) {
+  float* Wsl = Ss + 64 * 16;       // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
+
+  // cell-epilogue mapping: thread -> row rr, units u0, u0 + 1 of the tile
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
+  const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
+  const int j = nt * 16 + u0;
+  // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
+  //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
+  int64_t tk = tok[(int64_t)mc * tok_ld];
+
+  // ---- GEMM: this wave's K chunks, loads two chunks ahead ----
+  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
+  const int kc0 = wave * per;
+  const bf16x8* af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
+  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  floatx16 acc[2][2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) C1[(wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31)] = acc[0][0][r];
-  } else {
-    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
-    for (int i = tg; i < 2 * P * 4; i += 256) {
-      const float4 v = src[i];
-      float* d = Wsl + (i >> 2) * 17 + 4 * (i & 3);
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-  }
-  __syncthreads();
-  if (grp == 0) {
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int idx = (wm * 32 + acc_row(r, lane)) * CP + wn * 32 + (lane & 31);
-      Cs[idx] = acc[0][0][r] + C1[idx];
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][0][q] = af0[o];
+      fa[slot][1][q] = af1[o];
+      fw[slot][0][q] = wf0[o];
+      fw[slot][1][q] = wf1[o];
     }
-  }
-  __syncthreads();
-  if (grp == 0) {
-    const int rr = tg >> 2, u0 = (tg & 3) * 4, m = m0 + rr;
-    const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
-    int64_t tk = 1;  // <start> (adaptive_attention.py:187-190)
-    if (keys_prev) tk = key_token(keys_prev[mc]);
-    else if (tok_in) tk = tok_in[mc];
+  };
+  const int last = kc0 + per - 1;
+  asm volatile("" ::: "memory");
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
+  float2 ta[4], xa[4], sa, sb, cprev;
+  float4 wsv;
+  {
     tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
     const int N5 = 5 * H;
     const float* trow = table + tk * N5;
     const float* xrow = xg + (int64_t)mc * N5;
-    const float* cr = Cs + rr * CP;
-    const int j = nt * 16 + u0;
-    float4 pre[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const float4 a = *reinterpret_cast<const float4*>(trow + nt * 64 + g * 16 + u0);
-      const float4 b = *reinterpret_cast<const float4*>(xrow + nt * 64 + g * 16 + u0);
-      pre[g] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
     }
-    const float4 sa = *reinterpret_cast<const float4*>(trow + 4 * H + j);
-    const float4 sb = *reinterpret_cast<const float4*>(xrow + 4 * H + j);
-    const float4 cprev = *reinterpret_cast<const float4*>(c_in + (int64_t)mc * H + j);
-    float hn[4], cn[4], sn[4];
+    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+    sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
+    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)mc * H + j);
+    // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
+    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+    wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float gi = cr[0 + u0 + q] + f4c(pre[0], q);
-      const float gf = cr[16 + u0 + q] + f4c(pre[1], q);
-      const float gg = cr[32 + u0 + q] + f4c(pre[2], q);
-      const float go = cr[48 + u0 + q] + f4c(pre[3], q);
-      const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
-      cn[q] = f_ * f4c(cprev, q) + i_ * g_;
-      const float tc = tanhf(cn[q]);
-      hn[q] = o_ * tc;
-      sn[q] = sigmoidf_(f4c(sa, q) + f4c(sb, q)) * tc;
+  for (int i = 0; i < per; i += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
+      const int nk = kc0 + i + d + 2;
+      load(d, nk < last ? nk : last);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    *reinterpret_cast<float4*>(Hs + rr * 16 + u0) = make_float4(hn[0], hn[1], hn[2], hn[3]);
-    *reinterpret_cast<float4*>(Ss + rr * 16 + u0) = make_float4(sn[0], sn[1], sn[2], sn[3]);
-    if (m < B) {
-      *reinterpret_cast<float4*>(c_out + (int64_t)m * H + j) = make_float4(cn[0], cn[1], cn[2], cn[3]);
-      *reinterpret_cast<float4*>(h_out + (int64_t)m * H + j) = make_float4(hn[0], hn[1], hn[2], hn[3]);
-      *reinterpret_cast<float4*>(s_out + (int64_t)m * H + j) = make_float4(sn[0], sn[1], sn[2], sn[3]);
+  }
+  // ---- partial tiles -> LDS, fixed-tree sum into slot 0 ----
+  {
+    float* dst = Pt + wave * TS;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31)] = acc[a][c][r];
+  }
+  {  // transpose the W_g / W_s slice to [unit][j] (j = 98, 99 are zero)
+    const int jj = t >> 2, uq = (t & 3) * 4;
+    if (t < 2 * P * 4) {
+      Wsl[(uq + 0) * WSP + jj] = wsv.x; Wsl[(uq + 1) * WSP + jj] = wsv.y;
+      Wsl[(uq + 2) * WSP + jj] = wsv.z; Wsl[(uq + 3) * WSP + jj] = wsv.w;
+    } else if (t < 2 * P * 4 + 32) {
+      const int z = t - 2 * P * 4;  // 32 zeros: j = 98, 99 for 16 units
+      Wsl[(z >> 1) * WSP + 2 * P + (z & 1)] = 0.f;
     }
   }
   __syncthreads();
-  // partial projections: thread -> j = t % 128 (valid < 98), rows t/128, t/128 + 4, ...
-  const int jp = t & 127;
-  if (jp < 2 * P) {
-    float w[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) w[u] = Wsl[jp * 17 + u];
-    const float* vals = jp < P ? Hs : Ss;
-    for (int r = t >> 7; r < BM; r += 4) {
-      const int mr = m0 + r;
-      if (mr >= B) break;
-      float a = 0.f;
+  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
+    const int q = t + 512 * i, r = q >> 4, c4 = (q & 15) * 4;
+    const float* sp = Pt + r * CP + c4;
+    float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) a = __builtin_fmaf(vals[r * 16 + u], w[u], a);
-      part[((int64_t)mr * NTn + nt) * PART + jp] = a;
+    for (int w = 0; w < 8; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
+    float4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s01 = f4c(v[0], e) + f4c(v[1], e), s23 = f4c(v[2], e) + f4c(v[3], e);
+      const float s45 = f4c(v[4], e) + f4c(v[5], e), s67 = f4c(v[6], e) + f4c(v[7], e);
+      (&o.x)[e] = (s01 + s23) + (s45 + s67);
+    }
+    *reinterpret_cast<float4*>(Pt + r * CP + c4) = o;
+  }
+  __syncthreads();
+  {
+    const float* cr = Pt + rr * CP;
+    float hn[2], cn[2], sn[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float gi = cr[0 + u0 + q] + ((&ta[0].x)[q] + (&xa[0].x)[q]);
+      const float gf = cr[16 + u0 + q] + ((&ta[1].x)[q] + (&xa[1].x)[q]);
+      const float gg = cr[32 + u0 + q] + ((&ta[2].x)[q] + (&xa[2].x)[q]);
+      const float go = cr[48 + u0 + q] + ((&ta[3].x)[q] + (&xa[3].x)[q]);
+      const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+      cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
+      const float tc = tanhf(cn[q]);
+      hn[q] = o_ * tc;
+      sn[q] = sigmoidf_((&sa.x)[q] + (&sb.x)[q]) * tc;
+    }
+    *reinterpret_cast<float2*>(Hs + rr * 16 + u0) = make_float2(hn[0], hn[1]);
+    *reinterpret_cast<float2*>(Ss + rr * 16 + u0) = make_float2(sn[0], sn[1]);
+    if (m < B) {
+      *reinterpret_cast<float2*>(c_out + (int64_t)m * H + j) = make_float2(cn[0], cn[1]);
+      *reinterpret_cast<float2*>(h_out + (int64_t)m * H + j) = make_float2(hn[0], hn[1]);
+      *reinterpret_cast<float2*>(s_out + (int64_t)m * H + j) = make_float2(sn[0], sn[1]);
+      if (hsp_out) {
+        // next step's A fragments: k = j.. in chunk nt, lane (m % 32) + 32 * (u0 / 8), elements u0 % 8..
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 p0, p1, p2;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          __bf16 x0, x1, x2;
+          split3(hn[q], x0, x1, x2);
+          p0[q] = x0; p1[q] = x1; p2[q] = x2;
+        }
+        bf16x8* o = hsp_out + ((size_t)((m >> 5) * KC + nt) * 3) * 64 + (m & 31) + 32 * (u0 >> 3);
+        const int e = u0 & 7;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e) = p0;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e) = p1;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e) = p2;
+      }
     }
   }
+  __syncthreads();
+  // partial projections, four outputs j = 4 jq .. 4 jq + 3 of one row per task (float4 store):
+  // part[row][tile][j] = sum_{u < 16} (j < 49 ? h'_u : s_u) W[j][u], fma chain in u order
+  for (int task = t; task < BM * (WSP / 4); task += 512) {
+    const int r = task / (WSP / 4), jq = task % (WSP / 4);
+    const int mr = m0 + r;
+    if (mr < B) {
+      float4 hv[4], sv[4];
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        hv[u4] = *reinterpret_cast<const float4*>(Hs + r * 16 + 4 * u4);
+        sv[u4] = *reinterpret_cast<const float4*>(Ss + r * 16 + 4 * u4);
+      }
+      float acc4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float4 wv = *reinterpret_cast<const float4*>(Wsl + u * WSP + 4 * jq);
+        const float hu = f4c(hv[u >> 2], u & 3), su = f4c(sv[u >> 2], u & 3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc4[e] = __builtin_fmaf(4 * jq + e < P ? hu : su, f4c(wv, e), acc4[e]);
+      }
+      *reinterpret_cast<float4*>(part + ((int64_t)mr * NTn + nt) * PART + 4 * jq) =
+          make_float4(acc4[0], acc4[1], acc4[2], acc4[3]);
+    }
+  }
+}
+
+__global__ void k_fill_tok(int64_t* __restrict__ tok, int B, int64_t v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) tok[i] = v;
+}
+__global__ void k_key_ids(const uint64_t* __restrict__ keys, int B, int64_t* __restrict__ ids, int ld) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) ids[(int64_t)i * ld] = key_token(keys[i]);
+}
+
+// h [B][H] fp32 -> three bf16 planes in MFMA A-fragment order (see k_lstm); one thread per 8 values.
+__global__ void k_split_rows(const float* __restrict__ h, int B, int H, bf16x8* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (m, kc, half)
+  const int KC = H / 16;
+  if (i >= (int64_t)B * KC * 2) return;
+  const int hf = (int)(i & 1), kc = (int)((i >> 1) % KC), m = (int)((i >> 1) / KC);
+  const float* src = h + (int64_t)m * H + 16 * kc + 8 * hf;
+  bf16x8 p0, p1, p2;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    __bf16 x0, x1, x2;
+    split3(src[e], x0, x1, x2);
+    p0[e] = x0; p1[e] = x1; p2[e] = x2;
+  }
+  bf16x8* o = out + ((size_t)((m >> 5) * KC + kc) * 3) * 64 + (m & 31) + 32 * hf;
+  o[0] = p0;
+  o[64] = p1;
+  o[128] = p2;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1251,6 +1390,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
   hipLaunchKernelGGL(k_pack_wgs, dim3(H / 16), dim3(256), 0, s, w->att_affine_g_w, w->att_affine_s_w, H, base + L.wgs);
   hipLaunchKernelGGL(k_pack_w3, dim3((H / 32) * (C / 16)), dim3(64), 0, s, w->enc_affine_a_w, C,
                      reinterpret_cast<bf16x8*>(base + L.enc_w3));
+  hipLaunchKernelGGL(k_pack_w3, dim3((4 * H / 32) * (H / 16)), dim3(64), 0, s, base + L.whh, H,
+                     reinterpret_cast<bf16x8*>(base + L.whh3));
   return launch_status();
 }
 
@@ -1318,8 +1459,12 @@ struct Carver {
 
 struct StepWS {
   float *xg, *s, *u, *vwv, *part;
+  bf16x8* hsp;
   uint64_t* keys;
+  int64_t* tok0;
 };
+// split-h fragment buffer: rows padded to 32, 3 planes of bf16
+static size_t hsp_frags(const Layout& L, int B) { return (size_t)((B + 31) / 32) * (L.H / 16) * 3 * 64; }
 static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
   Carver c{base};
   StepWS w;
@@ -1328,7 +1473,9 @@ static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
   w.u = c.take<float>((size_t)B * L.H);
   w.vwv = c.take<float>((size_t)B * P * PP);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
+  w.hsp = c.take<bf16x8>(hsp_frags(L, B));
   w.keys = c.take<uint64_t>((size_t)B);
+  w.tok0 = c.take<int64_t>((size_t)B);
   *bytes = c.off;
   return w;
 }
@@ -1336,8 +1483,10 @@ static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
 struct DecodeWS {
   float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part;
   uint16_t* ub;
+  bf16x8* hsp[2];
   float4* summ;
   uint64_t* keys;
+  int64_t* tok0;
 };
 static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* bytes) {
   Carver c{base};
@@ -1356,8 +1505,10 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.unorm = c.take<float>((size_t)B);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
   w.ub = c.take<uint16_t>((size_t)B * L.H);
+  for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
+  w.tok0 = c.take<int64_t>((size_t)B);
   *bytes = c.off;
   return w;
 }
@@ -1378,15 +1529,23 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 
 
 // LSTM + attention for one step (shared by the step API and the greedy loop)
-static void lstm_atten_launch(const Layout& L, const MP& p, int B, const uint64_t* keys_prev, const int64_t* tok_in,
-                              const float* V, const float* vwv, const float* xg, const float* h_in, const float* c_in,
-                              float* h_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
+static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld,
+                              const float* V, const float* vwv, const float* xg, const bf16x8* hsp_in,
+                              const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
                               float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
                               const aa_trace* tr, int t, hipStream_t s) {
   const int H = L.H, MT = (B + 63) / 64;
   rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
-  hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16)), dim3(512), 0, s, B, H, L.V, keys_prev, tok_in, p.table, xg, h_in,
-                     c_in, p.whh, p.wgs, h_out, c_out, s_buf, part);
+#define AA_LSTM(H_)                                                                                        \
+  hipLaunchKernelGGL(k_lstm<H_>, dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, xg, hsp_in, \
+                     c_in, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part)
+  switch (H) {
+    case 256: AA_LSTM(256); break;
+    case 512: AA_LSTM(512); break;
+    case 768: AA_LSTM(768); break;
+    default: AA_LSTM(1024); break;
+  }
+#undef AA_LSTM
   rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
   rec(tr ? tr->atten_events : nullptr, 2 * t, s);
 #define AA_ATTEN(HPT_)                                                                                     \
@@ -1426,8 +1585,15 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   }
   gemm_bias(v_g, L.E, B, p.wvg, L.E, L.N5, L.E, p.bias5, w.xg, L.N5, s);
   AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)B * sizeof(uint64_t), s));
-  lstm_atten_launch(L, p, B, nullptr, tokens_in, V, VWv, w.xg, h_in, c_in, h_out, c_out, w.s, w.part, w.u, nullptr,
-                    nullptr, alpha, P, beta, 1, nullptr, 0, s);
+  hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, h_in, B,
+                     L.H, w.hsp);
+  const int64_t* tok = tokens_in;
+  if (!tok) {
+    hipLaunchKernelGGL(k_fill_tok, dim3((B + 255) / 256), dim3(256), 0, s, w.tok0, B, (int64_t)1);  // <start>
+    tok = w.tok0;
+  }
+  lstm_atten_launch(L, p, B, tok, 1, V, VWv, w.xg, w.hsp, c_in, h_out, nullptr, c_out, w.s, w.part, w.u,
+                    nullptr, nullptr, alpha, P, beta, 1, nullptr, 0, s);
   hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w,
                      p.mlp_b, scores, w.keys);
   hipLaunchKernelGGL(k_finalize, dim3((B + 255) / 256), dim3(256), 0, s, w.keys, B, 1, tokens_out);
@@ -1443,6 +1609,8 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
   const float* vwv = w.vwv + (size_t)r0 * P * PP;
   const float* xg = w.xg + (size_t)r0 * L.N5;
   float* hb[2] = {w.h[0] + (size_t)r0 * H, w.h[1] + (size_t)r0 * H};
+  const size_t fo = (size_t)(r0 / 32) * (H / 16) * 3 * 64;  // r0 is a multiple of 64
+  bf16x8* hs[2] = {w.hsp[0] + fo, w.hsp[1] + fo};
   float* cb[2] = {w.c[0] + (size_t)r0 * H, w.c[1] + (size_t)r0 * H};
   float* sb = w.s + (size_t)r0 * H;
   float* part = w.part + (size_t)r0 * (H / 16) * PART;
@@ -1455,9 +1623,11 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
   float* bl = beta ? beta + (size_t)r0 * T : nullptr;
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
-    const uint64_t* kprev = t ? w.keys + (size_t)(t - 1) * B + r0 : nullptr;
+    // token of step t-1: ids[:, t-1] (written by the previous step), <start> at t = 0
+    const int64_t* tok = t ? idsl + (t - 1) : w.tok0 + r0;
+    const int tok_ld = t ? T : 1;
     uint64_t* kt = w.keys + (size_t)t * B + r0;
-    lstm_atten_launch(L, p, Bl, kprev, nullptr, V, vwv, xg, hb[cur], cb[cur], hb[nxt], cb[nxt], sb, part, u,
+    lstm_atten_launch(L, p, Bl, tok, tok_ld, V, vwv, xg, hs[cur], cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, u,
                       exact ? nullptr : ub, exact ? nullptr : unorm, al ? al + (size_t)t * P : nullptr,
                       (int64_t)T * P, bl ? bl + t : nullptr, T, trace, t, s);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
@@ -1467,6 +1637,7 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
       hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, p.mlp_w, p.mlp_b,
                          nullptr, kt);
       rec(sev, 2 * t + 1, s);
+      hipLaunchKernelGGL(k_key_ids, dim3((Bl + 255) / 256), dim3(256), 0, s, kt, Bl, idsl + t, T);
     } else {
       hipLaunchKernelGGL(k_vscreen, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.H,
                          L.V, L.Vp, ub, unorm, p.mlp_wb, p.mlp_gs, p.mlp_b, summ);
@@ -1498,6 +1669,9 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, flags, s);
   if (rc) return rc;
+  hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
+                     L.H, w.hsp[0]);
+  hipLaunchKernelGGL(k_fill_tok, dim3((B + 255) / 256), dim3(256), 0, s, w.tok0, B, (int64_t)1);  // <start>
   // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
   int nl = n_lanes > 0 ? n_lanes : 1;
   const int tiles = (B + 63) / 64;
@@ -1536,10 +1710,6 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
       AA_TRY(hipEventDestroy(join[i]));
     }
     AA_TRY(hipEventDestroy(fork));
-  }
-  if (exact) {
-    const int64_t n = (int64_t)B * T;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.keys, B, T, ids);
   }
   return launch_status();
 }

@@ -23,8 +23,8 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
   uint64_t* kt = w.keys + B;
   auto launch = [&]() -> bool {
     if (!strcmp(which, "lstm")) {
-      hipLaunchKernelGGL(k_lstm, dim3(MT * (H / 16)), dim3(512), 0, s, B, H, L.V, kprev, nullptr, p.table, w.xg,
-                         w.h[0], w.c[0], p.whh, p.wgs, w.h[1], w.c[1], w.s, w.part);
+      hipLaunchKernelGGL(k_lstm<512>, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
     } else if (!strcmp(which, "atten")) {
       hipLaunchKernelGGL(k_atten<2>, dim3(B), dim3(256), 0, s, B, H / 16, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
                          (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm);
