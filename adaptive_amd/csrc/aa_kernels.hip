@@ -1399,14 +1399,36 @@ static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
   if (arr) (void)hipEventRecord((hipEvent_t)arr[i], s);
 }
 
+// Encoder tail.  With an aux stream, the a_g branch (k_avgpool -> k_enc_heads -> x_g GEMM: HBM- and
+// latency-bound) runs beside the V branch (k_enc_v3 -> VWv GEMM: MFMA-bound); both read only the
+// features, and `s` waits for aux before returning.
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
-                          hipStream_t s) {
+                          hipStream_t s, hipStream_t aux = nullptr) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
-  rec(ev, 0, s);
-  hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, feats, nch, a_g);
-  rec(ev, 1, s);
+  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t sa = s;
+  if (aux && aux != s) {
+    AA_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    AA_TRY(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    AA_TRY(hipEventRecord(fork, s));
+    AA_TRY(hipStreamWaitEvent(aux, fork, 0));
+    sa = aux;
+  }
+  rec(ev, 0, sa);
+  hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, sa, feats, nch, a_g);
+  rec(ev, 1, sa);
+  rec(ev, 4, sa);
+  {
+    const int MT = (B + 63) / 64, NTn = L.NHp / 64;
+    hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, sa, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
+                       v_g, h0, c0);
+  }
+  rec(ev, 5, sa);
+  rec(ev, 8, sa);
+  if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, sa);
+  rec(ev, 9, sa);
   rec(ev, 2, s);
   if (flags & AA_DECODE_FP32_ENCODER) {
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
@@ -1416,19 +1438,15 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     hipLaunchKernelGGL(k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_w3, p.enc_a_b, V);
   }
   rec(ev, 3, s);
-  rec(ev, 4, s);
-  {
-    const int MT = (B + 63) / 64, NTn = L.NHp / 64;
-    hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, s, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
-                       v_g, h0, c0);
-  }
-  rec(ev, 5, s);
   rec(ev, 6, s);
   if (VWv) gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
   rec(ev, 7, s);
-  rec(ev, 8, s);
-  if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, s);
-  rec(ev, 9, s);
+  if (join) {
+    AA_TRY(hipEventRecord(join, sa));
+    AA_TRY(hipStreamWaitEvent(s, join, 0));
+    AA_TRY(hipEventDestroy(join));
+    AA_TRY(hipEventDestroy(fork));
+  }
   return launch_status();
 }
 
@@ -1652,7 +1670,7 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
 
 static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
                        float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
-                       hipStream_t s, const aa_stream_t* lanes, int32_t n_lanes) {
+                       hipStream_t s, const aa_stream_t* lanes, int32_t n_lanes, hipStream_t aux = nullptr) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
@@ -1666,8 +1684,9 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   const MP p = resolve(m, L);
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
+  if (!aux && n_lanes > 1) aux = (hipStream_t)lanes[1];
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
-                      trace ? trace->encoder_events : nullptr, flags, s);
+                      trace ? trace->encoder_events : nullptr, flags, s, aux);
   if (rc) return rc;
   hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
                      L.H, w.hsp[0]);
@@ -1732,7 +1751,7 @@ int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int
 struct aa_decode_plan {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  hipStream_t cap = nullptr;
+  hipStream_t cap = nullptr, aux = nullptr;
   hipStream_t lanes[AA_MAX_LANES] = {};
   int n_lanes = 0;
 };
@@ -1744,6 +1763,7 @@ static void plan_free(aa_decode_plan* p) {
   for (int i = 0; i < p->n_lanes; ++i)
     if (p->lanes[i]) (void)hipStreamDestroy(p->lanes[i]);
   if (p->cap) (void)hipStreamDestroy(p->cap);
+  if (p->aux) (void)hipStreamDestroy(p->aux);
   delete p;
 }
 
@@ -1763,6 +1783,7 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   aa_decode_plan* p = new aa_decode_plan();
   hipError_t e = hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking);
   const int nl = n_lanes > 1 ? n_lanes : 0;
   for (int i = 0; e == hipSuccess && i < nl; ++i) {
     e = hipStreamCreateWithFlags(&p->lanes[i], hipStreamNonBlocking);
@@ -1774,7 +1795,7 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
     return (int)e;
   }
   rc = greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, nullptr, flags, p->cap,
-                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl);
+                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl, p->aux);
   e = hipStreamEndCapture(p->cap, &p->graph);
   if (rc == 0 && e != hipSuccess) rc = (int)e;
   if (rc == 0) {
