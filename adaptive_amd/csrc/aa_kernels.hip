@@ -267,7 +267,8 @@ __global__ __launch_bounds__(256) void k_enc_v(const float* __restrict__ feats, 
 //   A: read from the NCHW feature map (row m = b*49 + p, column = channel; lanes over consecutive
 //      rows -> contiguous addresses), split in registers, staged in LDS as three bf16 planes
 //      [row][k] with an 80-B pitch (conflict-free ds_read_b128 / ds_write_b128).
-// Tile 128 x 128 per 256-thread workgroup; each wave owns 64 x 64 (2 x 2 blocks of 32 x 32);
+// Tile 128 x 128 per 256-thread workgroup; each wave owns 128 x 32 (4 blocks of 32 x 32: its own
+// W columns, the A rows shared through LDS);
 // K in stages of 32 (two k16 MFMA steps), A double-buffered in LDS, A and W prefetched a stage
 // ahead in registers.
 // ---------------------------------------------------------------------------------------------
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
   const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN, KC = C / 16;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int mt = L / NTn, nt = L % NTn;  // n fastest: the A tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 31, lh = lane >> 5;
   // A staging: thread -> row r (0..127), k-half kh: k = 16 kh + i, i < 16, of each 32-stage
   const int r = t & (EV_BM - 1), kh = t >> 7;
@@ -296,34 +297,27 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
   m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
   const int bi = m / P, pi = m - bi * P;
   const float* arow = feats + (int64_t)bi * C * P + pi + (int64_t)(16 * kh) * P;
-  // W fragments of this wave: n-blocks nb0 + c (c = 0, 1)
-  const int nb0 = (nt * EV_BN + wn * 64) / 32;
+  // W fragments of this wave: its own 32-column block (no fragment is loaded by two waves)
+  const int nb0 = (nt * EV_BN + wave * 32) / 32;
   const bf16x8* wf0 = W3 + (size_t)nb0 * KC * 3 * 64 + lane;
-  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
   float ra[16];
-  bf16x8 wa[2][2][3], wb[2][2][3];  // [sub][c][q], two stages in flight
-  floatx16 acc[2][2];
+  bf16x8 wa[2][3], wb[2][3];  // [sub][q], two stages in flight
+  floatx16 acc[4];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.f;
+    for (int i = 0; i < 16; ++i) acc[a][i] = 0.f;
 
   auto gload_a = [&](int s) {
     const float* src = arow + (int64_t)(EV_BK * s) * P;
 #pragma unroll
     for (int i = 0; i < 16; ++i) ra[i] = src[i * P];
   };
-  auto gload_w = [&](int s, bf16x8 (&w)[2][2][3]) {
+  auto gload_w = [&](int s, bf16x8 (&w)[2][3]) {
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const size_t o = ((size_t)(2 * s + sub) * 3 + q) * 64;
-        w[sub][0][q] = wf0[o];
-        w[sub][1][q] = wf1[o];
-      }
+      for (int q = 0; q < 3; ++q) w[sub][q] = wf0[((size_t)(2 * s + sub) * 3 + q) * 64];
   };
   auto lstore_a = [&](int buf) {
     bf16x8 h[2], md[2], lo[2];
@@ -343,28 +337,24 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
       *reinterpret_cast<bf16x8*>(&As[buf][2][o + 8 * j]) = lo[j];
     }
   };
-  auto compute = [&](int buf, const bf16x8 (&w)[2][2][3]) {
+  auto compute = [&](int buf, const bf16x8 (&w)[2][3]) {
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      bf16x8 fa[2][3];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 4; ++a) {
+        bf16x8 fa[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          fa[a][q] = *reinterpret_cast<const bf16x8*>(&As[buf][q][(wm * 64 + a * 32 + li) * EV_LD + 16 * sub + 8 * lh]);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          floatx16 x = acc[a][c];
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], w[sub][c][0], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], w[sub][c][1], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][2], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], w[sub][c][0], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][1], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], w[sub][c][0], x, 0, 0, 0);
-          acc[a][c] = x;
-        }
+          fa[q] = *reinterpret_cast<const bf16x8*>(&As[buf][q][(a * 32 + li) * EV_LD + 16 * sub + 8 * lh]);
+        floatx16 x = acc[a];
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], w[sub][0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], w[sub][1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], w[sub][2], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], w[sub][0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], w[sub][1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], w[sub][0], x, 0, 0, 0);
+        acc[a] = x;
+      }
     }
   };
 
@@ -399,19 +389,15 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
   }
-  const int colb = nt * EV_BN + wn * 64 + li;
+  const int col = nt * EV_BN + wave * 32 + li;
+  const float bv = bias[col];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int col = colb + 32 * c;
-    const float bv = bias[col];
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = mt * EV_BM + wm * 64 + a * 32 + acc_row(i, lane);
-        if (row < M) V[(int64_t)row * H + col] = reluf_(acc[a][c][i] + bv);
-      }
-  }
+    for (int i = 0; i < 16; ++i) {
+      const int row = mt * EV_BM + a * 32 + acc_row(i, lane);
+      if (row < M) V[(int64_t)row * H + col] = reluf_(acc[a][i] + bv);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
