@@ -179,6 +179,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
   return k;
 }
 
+// Element (row m, k) of a [rows][K] bf16 matrix stored in MFMA-fragment order (32-row blocks x
+// 16-wide k chunks x 64 lanes x 8): lane l of a fragment holds row (l & 31), k = 8 (l >> 5) + e.
+__device__ __forceinline__ int64_t frag_off(int m, int k, int K) {
+  return (((int64_t)(m >> 5) * (K >> 4) + (k >> 4)) * 64 + (m & 31) + 32 * ((k >> 3) & 1)) * 8 + (k & 7);
+}
+
 // fp32 -> bf16, round to nearest even (finite inputs)
 __device__ __forceinline__ uint16_t f2bf(float x) {
   const uint32_t u = __float_as_uint(x);
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __re
     const float u = chat + hv[i];
     nsq = __builtin_fmaf(u, u, nsq);
     u_out[(int64_t)b * H + d] = u;
-    if (ub_out) ub_out[(int64_t)b * H + d] = f2bf(u);
+    if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
   }
   if (unorm) {
     nsq = wave_sum(nsq);
@@ -887,44 +893,43 @@ __device__ __forceinline__ void screen_bfly(uint32_t (&k1)[16], uint32_t (&k2)[1
 // Screen tile: 128 rows x 128 columns per workgroup, K in 64-wide bf16 steps staged through
 // double-buffered LDS (global->register prefetch of step k+1 under the MFMAs of step k); each
 // wave owns 64 x 64 = 2 x 2 blocks of v_mfma_f32_32x32x16_bf16.
-constexpr int SC_BM = 128, SC_BN = 128, SC_BK = 64, SC_LD = SC_BK + 8;  // LDS row pitch in bf16
-__global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp, const uint16_t* __restrict__ ub,
-                                                    const float* __restrict__ unorm, const uint16_t* __restrict__ wb,
+// Screen tile: 64 rows x 64 columns per 256-thread workgroup.  Both operands are bf16 in
+// MFMA-fragment order (u written so by k_atten, W_m at pack time), so wave w loads every fragment
+// of its quarter of K -- 2 x 2 blocks x H/64 chunks -- straight into VGPRs in one round trip,
+// computes the whole 64x64 tile over that quarter, and the four partial tiles meet in LDS
+// ((p0 + p2) + (p1 + p3)); then each wave takes one 32x32 block for the epilogue.  (The screen's
+// error bound holds for any fp32 summation order.)
+constexpr int SC_BM = 64, SC_BN = 64, SC_PT = 64 * 68;  // partial tile, pitch 68 floats
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                    const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
                                                     const float2* __restrict__ gs, const float* __restrict__ bias,
                                                     float4* __restrict__ summ) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (SC_BM + SC_BN) * SC_LD];
+  constexpr int KC = H / 16, KW = KC / 4;  // k16 chunks per wave
+  __shared__ __attribute__((aligned(16))) float Pt[2 * SC_PT];
   __shared__ float un_s[SC_BM];
   const int NTn = Vp / VS_TILE, NTs = Vp / SC_BN, MT = (B + SC_BM - 1) / SC_BM;
   const int L = xcd_remap(blockIdx.x, MT * NTs);
-  const int nt = L / MT, mt = L % MT;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn_ = wave & 1;
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int m0 = mt * SC_BM, n0 = nt * SC_BN;
-  if (t < SC_BM) un_s[t] = unorm[m0 + t < B ? m0 + t : B - 1];
-  // staging map: 16-B chunk q = t + 256 i (i < 4) -> row (t >> 3) + 32 i, chunk t & 7 (8 bf16)
-  const int sr = t >> 3, sc = t & 7;
-  int64_t aoff[4];
+  const bf16x8* a0 = ua + ((size_t)(m0 >> 5) * KC + wave * KW) * 64 + lane;
+  const bf16x8* w0 = wf + ((size_t)(n0 >> 5) * KC + wave * KW) * 64 + lane;
+  bf16x8 fa[KW][2], fw[KW][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + sr + 32 * i;
-    aoff[i] = (int64_t)(m < B ? m : B - 1) * H + 8 * sc;  // clamp, never zero (rows >= B are not stored)
-  }
-  const uint16_t* wbase = wb + (int64_t)(n0 + sr) * H + 8 * sc;
-  u32x4 ra[4], rw[4];
-#define SC_GLOAD(ks)                                                                                  \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                     \
-    ra[i] = *reinterpret_cast<const u32x4*>(ub + aoff[i] + (ks) * SC_BK);                              \
-    rw[i] = *reinterpret_cast<const u32x4*>(wbase + (int64_t)32 * i * H + (ks) * SC_BK);               \
-  }
-#define SC_LSTORE(buf)                                                                                \
-  {                                                                                                   \
-    uint16_t* As_ = lds + (buf) * (SC_BM + SC_BN) * SC_LD;                                            \
-    uint16_t* Ws_ = As_ + SC_BM * SC_LD;                                                              \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                   \
-      *reinterpret_cast<u32x4*>(As_ + (sr + 32 * i) * SC_LD + 8 * sc) = ra[i];                          \
-      *reinterpret_cast<u32x4*>(Ws_ + (sr + 32 * i) * SC_LD + 8 * sc) = rw[i];                          \
-    }                                                                                                 \
-  }
+  for (int c = 0; c < KW; ++c)
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      fa[c][x] = a0[((size_t)x * KC + c) * 64];
+      fw[c][x] = w0[((size_t)x * KC + c) * 64];
+    }
+  // epilogue operands, loaded behind the fragments (their latency hides under the MFMAs)
+  const float unv = unorm[m0 + (t & 63) < B ? m0 + (t & 63) : B - 1];
+  const int wm = wave >> 1, wn_ = wave & 1;
+  const int col = n0 + wn_ * 32 + li;
+  const float bv = bias[col];
+  const float2 gsv = gs[(n0 + wn_ * 32) / VS_TILE];
   floatx16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -932,53 +937,69 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp,
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-  const int nk = H / SC_BK;
-  SC_GLOAD(0)
-  SC_LSTORE(0)
+#pragma unroll
+  for (int c = 0; c < KW; ++c)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int x = 0; x < 2; ++x) acc[a][x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][a], fw[c][x], acc[a][x], 0, 0, 0);
+  // partial tiles meet in LDS as [col][row] (pitch 68): a lane's 4 consecutive rows are one
+  // 16-B access.  Waves 2, 3 -> LDS; waves 0, 1 add them; wave 1 -> LDS; wave 0 adds -> slot 0.
+  auto put = [&](float* dst) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(dst + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[a][x][4 * r4], acc[a][x][4 * r4 + 1], acc[a][x][4 * r4 + 2], acc[a][x][4 * r4 + 3]);
+  };
+  auto add = [&](const float* src) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh);
+          acc[a][x][4 * r4] += v.x; acc[a][x][4 * r4 + 1] += v.y;
+          acc[a][x][4 * r4 + 2] += v.z; acc[a][x][4 * r4 + 3] += v.w;
+        }
+  };
+  if (wave >= 2) put(Pt + (wave - 2) * SC_PT);
+  if (t < SC_BM) un_s[t] = unv;
   __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    const bool more = ks + 1 < nk;
-    if (more) { SC_GLOAD(ks + 1) }
-    const uint16_t* As = lds + buf * (SC_BM + SC_BN) * SC_LD;
-    const uint16_t* Ws = As + SC_BM * SC_LD;
-#pragma unroll
-    for (int kk = 0; kk < SC_BK / 16; ++kk) {
-      bf16x8 fa[2], fw[2];
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-        fa[a] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + a * 32 + li) * SC_LD + 16 * kk + 8 * lh);
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        fw[c] = *reinterpret_cast<const bf16x8*>(Ws + (wn_ * 64 + c * 32 + li) * SC_LD + 16 * kk + 8 * lh);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fw[c], acc[a][c], 0, 0, 0);
-    }
-    if (more) SC_LSTORE(buf ^ 1)
-    __syncthreads();
+  if (wave < 2) add(Pt + wave * SC_PT);  // p0 + p2, p1 + p3
+  __syncthreads();
+  if (wave == 1) put(Pt);
+  __syncthreads();
+  if (wave == 0) {
+    add(Pt);                              // (p0 + p2) + (p1 + p3)
+    put(Pt);
   }
-#undef SC_GLOAD
-#undef SC_LSTORE
+  __syncthreads();
+  // each wave: one 32x32 block (wm, wn_) of the summed tile, back in MFMA C layout
+  floatx16 blk;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const float4 v = *reinterpret_cast<const float4*>(Pt + (wn_ * 32 + li) * 68 + wm * 32 + 8 * r4 + 4 * lh);
+    blk[4 * r4] = v.x; blk[4 * r4 + 1] = v.y; blk[4 * r4 + 2] = v.z; blk[4 * r4 + 3] = v.w;
+  }
   // epilogue: screened logits A = acc + b -> order-preserving u32 keys whose low 5 bits are replaced
   // by the column's position in its granule (truncation < 32 ulp, covered by EPS_ABS), then per
   // (row, 32-column granule) a transposing butterfly over the 32 lanes that hold the granule's
   // columns (levels 16, 8, 4, 2 each halve the rows a lane carries; level 1 completes): k1 = max
   // key (value and arg-max), k2 = second largest.  The bound E of the granule is applied last.
-  const int G0 = (n0 + wn_ * 64) / VS_TILE;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int col = n0 + wn_ * 64 + c * 32 + li;
+  const int G0 = (n0 + wn_ * 32) / VS_TILE;
+  {
+    const int c = 0, a = wm;
     const bool valid = col < V;
-    const float bv = bias[col];
-    const float2 gsv = gs[G0 + c];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    {
       uint32_t k1[16], k2[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint32_t key = order_key(acc[a][c][r] + bv);
+        const uint32_t key = order_key(blk[r] + bv);
         k1[r] = valid ? (key & ~31u) | (uint32_t)li : 0u;
         k2[r] = 0u;
       }
@@ -991,7 +1012,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int H, int V, int Vp,
       const uint32_t lo = k1[0] > r1 ? r1 : k1[0], h2 = k2[0] > r2 ? k2[0] : r2;
       const uint32_t m2 = lo > h2 ? lo : h2;
       const int rr = (li >> 1) & 15;  // this lane pair now holds row acc_row(rr) of the block
-      const int rl = wm * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      const int rl = a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
       const int row = m0 + rl;
       if (!(li & 1) && row < B) {
         float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
@@ -1239,7 +1260,7 @@ __global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, uint16_t* 
   float s = 0.f;
   for (int k = lane; k < H; k += 64) {
     const float x = n < V ? w[(int64_t)n * H + k] : 0.f;
-    wb[(int64_t)n * H + k] = f2bf(x);
+    wb[frag_off(n, k, H)] = f2bf(x);
     s += x * x;
   }
   s = wave_sum(s);
@@ -1468,7 +1489,8 @@ struct StepWS {
   int64_t* tok0;
 };
 // split-h fragment buffer: rows padded to 32, 3 planes of bf16
-static size_t hsp_frags(const Layout& L, int B) { return (size_t)((B + 31) / 32) * (L.H / 16) * 3 * 64; }
+// (rows padded to whole 64-row tiles: k_lstm reads its tile's two row blocks)
+static size_t hsp_frags(const Layout& L, int B) { return (size_t)((B + 63) / 64) * 2 * (L.H / 16) * 3 * 64; }
 static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
   Carver c{base};
   StepWS w;
@@ -1508,7 +1530,7 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.u = c.take<float>((size_t)B * L.H);
   w.unorm = c.take<float>((size_t)B);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
-  w.ub = c.take<uint16_t>((size_t)B * L.H);
+  w.ub = c.take<uint16_t>((size_t)((B + 63) / 64) * 64 * L.H);  // fragment order, 64-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
@@ -1643,8 +1665,17 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
       rec(sev, 2 * t + 1, s);
       hipLaunchKernelGGL(k_key_ids, dim3((Bl + 255) / 256), dim3(256), 0, s, kt, Bl, idsl + t, T);
     } else {
-      hipLaunchKernelGGL(k_vscreen, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.H,
-                         L.V, L.Vp, ub, unorm, p.mlp_wb, p.mlp_gs, p.mlp_b, summ);
+#define AA_SCREEN(H_)                                                                                    \
+  hipLaunchKernelGGL(k_vscreen<H_>, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.V, \
+                     L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                        \
+                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
+      switch (H) {
+        case 256: AA_SCREEN(256); break;
+        case 512: AA_SCREEN(512); break;
+        case 768: AA_SCREEN(768); break;
+        default: AA_SCREEN(1024); break;
+      }
+#undef AA_SCREEN
       rec(sev, 2 * t + 1, s);
       rec(rev, 2 * t, s);
       hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,

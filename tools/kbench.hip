@@ -29,8 +29,9 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
       hipLaunchKernelGGL(k_atten<2>, dim3(B), dim3(256), 0, s, B, H / 16, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
                          (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm);
     } else if (!strcmp(which, "vscreen")) {
-      hipLaunchKernelGGL(k_vscreen, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.H, L.V,
-                         L.Vp, w.ub, w.unorm, p.mlp_wb, p.mlp_gs, p.mlp_b, w.summ);
+      hipLaunchKernelGGL(k_vscreen<512>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V,
+                         L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,
+                         reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ);
     } else if (!strcmp(which, "vrescore")) {
       hipLaunchKernelGGL(k_vrescore, dim3(B), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
                          (int64_t*)nullptr, T, t);
