@@ -416,10 +416,72 @@ class Encoder2Decoder(nn.Module):
         _lib.check(rc, "vocab_logits")
         return out
 
+    # ---- Encoder2Decoder.forward (baseline_attention.py:206-230): teacher-forced training ------
     def forward(self, images, captions, lengths):
-        raise NotImplementedError(
-            "adaptive_amd: teacher-forced Encoder2Decoder.forward (training, baseline_attention.py:206-230) is "
-            "SURVEY.md §8f row 1 and not built yet; use sampler() for decoding.")
+        """Teacher-forced forward -> ``PackedSequence`` of the scores, exactly as the reference's
+        ``pack_padded_sequence(scores, lengths, batch_first=True)``; differentiable w.r.t. every
+        parameter (HIP forward and backward kernels, C-ABI ``aa_train_*``), so train.py's closure
+        (CrossEntropyLoss on ``packed[0]``, ``loss.backward()``, clip_grad_norm_, optimizer.step)
+        runs unchanged.  ``images`` are post-trunk features [B,2048,7,7]."""
+        from torch.nn.utils.rnn import PackedSequence
+        images = self._check_images(images)
+        lengths = [int(n) for n in (lengths.tolist() if torch.is_tensor(lengths) else lengths)]
+        B = images.size(0)
+        if captions.dim() != 2 or captions.size(0) != B or len(lengths) != B:
+            raise ValueError("captions must be [B, L] and lengths a list of B ints")
+        if any(n < 1 for n in lengths) or any(lengths[i] < lengths[i + 1] for i in range(B - 1)):
+            raise ValueError("lengths must be positive and sorted in decreasing order (pack_padded_sequence)")
+        T = lengths[0]
+        if T > captions.size(1):
+            raise ValueError("lengths exceed the caption width")
+        dev = images.device
+        caps = captions.to(device=dev, dtype=torch.int64).contiguous()
+        len_dev = torch.tensor(lengths, dtype=torch.int32, device=dev)
+        batch_sizes = torch.tensor([sum(1 for n in lengths if n > t) for t in range(T)], dtype=torch.int64)
+        params = [dict(self.named_parameters())[k] for _, k in _lib.WEIGHT_FIELDS]
+        data = _TeacherForced.apply(self, images, caps, len_dev, sum(lengths), T, *params)
+        return PackedSequence(data, batch_sizes)
+
+
+class _TeacherForced(torch.autograd.Function):
+    """HIP teacher-forced forward / backward (aa_train_forward / aa_train_backward).  The workspace
+    of the forward call carries the activations to the backward call."""
+
+    @staticmethod
+    def forward(ctx, owner, images, caps, len_dev, N, T, *params):
+        lib = _lib.load()
+        d = owner._c_dims()
+        B = images.size(0)
+        nbytes = lib.aa_train_workspace_bytes(d, B, T)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=images.device)
+        scores = torch.empty(N, owner.dims.vocab, device=images.device)
+        w = _lib.RefWeights(*[p.data_ptr() for p in params])
+        with torch.cuda.device(images.device):
+            rc = lib.aa_train_forward(w, d, images.data_ptr(), B, T, caps.data_ptr(), caps.stride(0),
+                                      len_dev.data_ptr(), scores.data_ptr(), N, ws.data_ptr(), nbytes,
+                                      _lib.stream_handle())
+        _lib.check(rc, "train_forward")
+        ctx.owner, ctx.ws, ctx.N, ctx.T = owner, ws, N, T
+        ctx.save_for_backward(images, caps, len_dev, *params)
+        return scores
+
+    @staticmethod
+    def backward(ctx, dscores):
+        lib = _lib.load()
+        images, caps, len_dev, *params = ctx.saved_tensors
+        owner = ctx.owner
+        B = images.size(0)
+        dscores = dscores.contiguous().float()
+        grads = [torch.empty_like(p) for p in params]
+        w = _lib.RefWeights(*[p.data_ptr() for p in params])
+        g = _lib.RefWeights(*[t.data_ptr() for t in grads])
+        with torch.cuda.device(images.device):
+            rc = lib.aa_train_backward(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(), caps.stride(0),
+                                       len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g, ctx.ws.data_ptr(),
+                                       ctx.ws.numel(), _lib.stream_handle())
+        _lib.check(rc, "train_backward")
+        ctx.ws = None
+        return (None, None, None, None, None, None, *grads)
 
 
 def synthetic_features(B: int, device, seed: int = 0, row0: int = 0, dims: Dims = Dims()) -> torch.Tensor:

@@ -26,17 +26,11 @@
 #include <stdint.h>
 #include <string.h>
 
-#include "adaptive_amd.h"
-#include "aa_gemm.hpp"
+#include "aa_common.hpp"
 
 namespace aa {
 
-constexpr int P = 49;          // attention width == 7x7 spatial locations (adaptive_attention.py:16-19)
-constexpr int PP = 64;         // padded attention width (VWv row pitch, W_v rows)
-constexpr int MAX_H = 1024;    // k_atten keeps h and s rows in LDS
 constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Vocab-screen error bound.  For one logit, the fp32 path (k_vocab / k_vrescore) computes
 // L = fl(sum_k u_k w_k) + b and the screen computes A = fl(sum_k bf16(u_k) bf16(w_k)) + b.
@@ -133,19 +127,6 @@ static MP resolve(const aa_model* m, const Layout& L) {
 // ---------------------------------------------------------------------------------------------
 // small math helpers (accurate libm: expf/tanhf from the device library, no fast-math)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-__device__ __forceinline__ float reluf_(float x) { return x < 0.f ? 0.f : x; }
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
 
 // Argmax key: larger logit wins; on equal logits the smaller vocab index wins (torch max(2)[1]
 // returns the first maximal index, adaptive_attention.py:201).
@@ -1296,18 +1277,8 @@ __global__ void k_synth_uniform(float* __restrict__ dst, int64_t n, uint64_t key
 // =============================================================================================
 using namespace aa;
 
-#define AA_TRY(expr)                           \
-  do {                                         \
-    hipError_t e_ = (expr);                    \
-    if (e_ != hipSuccess) return (int)e_;      \
-  } while (0)
-
-static int launch_status() {
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? AA_OK : (int)e;
-}
-
-static bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+static int launch_status() { return aa_launch_status(); }
+static bool al16(const void* p) { return aa_al16(p); }
 
 static void gemm_bias(const float* A, int lda, int M, const float* W, int ldw, int N, int K, const float* bias, float* C,
                       int64_t ldc, hipStream_t s) {
@@ -1875,3 +1846,6 @@ int aa_synth_uniform(float* dst, int64_t n, uint64_t key, int64_t start, double 
                      (hipStream_t)stream, dst, n, key, start, lo, hi - lo, plain);
   return launch_status();
 }
+
+// teacher-forced training step (same translation unit: reuses the encoder kernels)
+#include "aa_train.hip"

@@ -1,0 +1,707 @@
+// aa_train.hip — teacher-forced training step of Encoder2Decoder (forward + backward), compiled
+// into the same translation unit as aa_kernels.hip (included at its end; it reuses k_avgpool and
+// k_enc_v).  Reference: baseline_attention.py:206-230 (forward), 148-194 (Decoder), 36-62
+// (AttentiveCNN tail); adaptive_attention.py:26-58 (Atten), 62-85 (Sentinel), 110-134
+// (AdaptiveBlock); train.py:101,197-219 (packed targets, CrossEntropyLoss, backward).
+//
+// Layout: every per-step array is t-major ([T][B][...], row r = t * B + b), so the LSTM step t
+// works on rows [tB, (t+1)B) and pack_padded_sequence's packed rows (t-major over b < batch
+// size of t; lengths sorted descending) are a monotone subset of the rows.
+//
+// Arithmetic: fp32 throughout.  GEMMs run on the generic fp32-MFMA tile kernel k_tgemm below
+// (operands in any of the layouts the backward pass needs, bounds-checked, fixed accumulation
+// order); everything else is elementwise or one-workgroup-per-row / per-image kernels with fixed
+// reduction orders, so a training step is deterministic run to run.  The cross-entropy loss is
+// the caller's (train.py computes it on the packed scores): backward starts from dL/dscores.
+
+namespace aa {
+
+// ---------------------------------------------------------------------------------------------
+// generic GEMM: C[M, N] (+)= act(sum_k A(m, k) W(n, k) + bias[n] + bias2[n])
+//   A(m, k) = at ? A[k lda + m] : A[row(m) lda + k]        row(m) = arow ? arow[m] : m
+//   W(n, k) = wm == 0 : W[n ldw + k]
+//             wm == 1 : W[k ldw + n]
+//             wm == 2 : NCHW feature map [B][C][49] read as the [B*49, C] row matrix transposed:
+//                       W(n = c, k = b*49 + p) = W[b*ldw*49 + c*49 + p]   (ldw = C)
+//   C row m -> crow ? crow[m] : m
+// 64x64 tiles, 256 threads (2 x 2 waves of 32x32), BK = 32 through double-buffered LDS, the same
+// k order as aa_gemm.hpp (lanes 0-31: k = s, lanes 32-63: k = 16 + s of each step).
+// ---------------------------------------------------------------------------------------------
+struct TG {
+  int M, N, K;
+  const float* A;
+  int64_t lda;
+  const int* arow;
+  int at;
+  const float* W;
+  int64_t ldw;
+  int wm;
+  float* C;
+  int64_t ldc;
+  const int* crow;
+  const float* bias;
+  const float* bias2;
+  int accumulate;
+  int act;  // 0 none, 1 relu, 2 tanh
+};
+
+__global__ __launch_bounds__(256) void k_tgemm(TG g) {
+  __shared__ __attribute__((aligned(16))) float lds[2][2][64 * LDK];
+  const int tilesN = (g.N + 63) / 64;
+  const int mt = blockIdx.x / tilesN, nt = blockIdx.x % tilesN;
+  const int m0 = mt * 64, n0 = nt * 64;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wmv = wave >> 1, wnv = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  float ra[8], rw[8];
+  auto gload = [&](int k0) {
+    if (!g.at) {  // 4 threads per row, 8 consecutive k each
+      const int r = t >> 2, kq = (t & 3) * 8, m = m0 + r;
+      const int64_t base = (int64_t)(m < g.M ? (g.arow ? g.arow[m] : m) : 0) * g.lda;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + kq + i;
+        ra[i] = (m < g.M && k < g.K) ? g.A[base + k] : 0.f;
+      }
+    } else {  // 8 threads per k, 8 consecutive m each
+      const int k = k0 + (t >> 3), mq = (t & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + mq + i;
+        ra[i] = (m < g.M && k < g.K) ? g.A[(int64_t)k * g.lda + m] : 0.f;
+      }
+    }
+    if (g.wm == 1) {
+      const int k = k0 + (t >> 3), nq = (t & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = n0 + nq + i;
+        rw[i] = (n < g.N && k < g.K) ? g.W[(int64_t)k * g.ldw + n] : 0.f;
+      }
+    } else {
+      const int r = t >> 2, kq = (t & 3) * 8, n = n0 + r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + kq + i;
+        float v = 0.f;
+        if (n < g.N && k < g.K) {
+          if (g.wm == 0) v = g.W[(int64_t)n * g.ldw + k];
+          else v = g.W[((int64_t)(k / P) * g.ldw + n) * P + (k % P)];
+        }
+        rw[i] = v;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    float* As = lds[buf][0];
+    float* Ws = lds[buf][1];
+    if (!g.at) {
+      const int r = t >> 2, kq = (t & 3) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) As[r * LDK + kq + i] = ra[i];
+    } else {
+      const int k = t >> 3, mq = (t & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) As[(mq + i) * LDK + k] = ra[i];
+    }
+    if (g.wm == 1) {
+      const int k = t >> 3, nq = (t & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Ws[(nq + i) * LDK + k] = rw[i];
+    } else {
+      const int r = t >> 2, kq = (t & 3) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Ws[r * LDK + kq + i] = rw[i];
+    }
+  };
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int nk = (g.K + BK - 1) / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload((ks + 1) * BK);
+    const float* As = lds[buf][0];
+    const float* Ws = lds[buf][1];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 a = *reinterpret_cast<const float4*>(As + (wmv * 32 + li) * LDK + 16 * lh + 4 * s4);
+      const float4 w = *reinterpret_cast<const float4*>(Ws + (wnv * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a, j), f4c(w, j), acc, 0, 0, 0);
+    }
+    if (ks + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  const int col = n0 + wnv * 32 + li;
+  if (col >= g.N) return;
+  const float bv = (g.bias ? g.bias[col] : 0.f) + (g.bias2 ? g.bias2[col] : 0.f);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wmv * 32 + acc_row(r, lane);
+    if (m >= g.M) continue;
+    float v = acc[r] + bv;
+    if (g.act == 1) v = reluf_(v);
+    else if (g.act == 2) v = tanhf(v);
+    float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
+    *dst = g.accumulate ? *dst + v : v;
+  }
+}
+
+// C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites
+static void tgemm(hipStream_t s, int M, int N, int K, const float* A, int64_t lda, int at, const float* W, int64_t ldw,
+                  int wm, float* C, int64_t ldc, int accumulate = 0, const float* bias = nullptr,
+                  const float* bias2 = nullptr, int act = 0, const int* arow = nullptr, const int* crow = nullptr) {
+  if (M <= 0 || N <= 0) return;
+  TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act};
+  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  hipLaunchKernelGGL(k_tgemm, dim3(tiles), dim3(256), 0, s, g);
+}
+
+// column sums: out[n] (+)= sum_m X[m ldx + n] over m in order (deterministic)
+__global__ void k_colsum(const float* __restrict__ X, int M, int N, int64_t ldx, float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int m = 0; m < M; ++m) s += X[(int64_t)m * ldx + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward pieces
+// ---------------------------------------------------------------------------------------------
+// X[t B + b] = [embed[tok[b][t]]; v_g[b]]  (baseline_attention.py:151-154)
+__global__ void k_tr_x(const int64_t* __restrict__ tok, int tld, const float* __restrict__ embed, int V, int E,
+                       const float* __restrict__ vg, int B, int T, float* __restrict__ X) {
+  const int r = blockIdx.x, t = r / B, b = r % B;
+  int64_t tk = tok[(int64_t)b * tld + t];
+  tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    X[(int64_t)r * 2 * E + e] = embed[tk * E + e];
+    X[(int64_t)r * 2 * E + E + e] = vg[(int64_t)b * E + e];
+  }
+}
+
+// LSTM cell of step t (torch gate order i, f, g, o): gates = G4 (h W_hh^T) + PRE (x W_ih^T + b)
+__global__ void k_tr_cell(const float* __restrict__ G4, const float* __restrict__ PRE, int ldp,
+                          const float* __restrict__ c_prev, int B, int H, float* __restrict__ h_out,
+                          float* __restrict__ c_out, float* __restrict__ GA) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * H) return;
+  const int b = (int)(i / H), j = (int)(i % H);
+  const float* g = G4 + (int64_t)b * 4 * H;
+  const float* p = PRE + (int64_t)b * ldp;
+  const float gi = g[j] + p[j], gf = g[H + j] + p[H + j], gg = g[2 * H + j] + p[2 * H + j],
+              go = g[3 * H + j] + p[3 * H + j];
+  const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+  const float c = f_ * c_prev[i] + i_ * g_;
+  c_out[i] = c;
+  h_out[i] = o_ * tanhf(c);
+  float* ga = GA + (int64_t)b * 4 * H;
+  ga[j] = i_; ga[H + j] = f_; ga[2 * H + j] = g_; ga[3 * H + j] = o_;
+}
+
+// sentinel: SG = sigmoid(x W_x^T + h_{t-1} W_h^T) (pre-activation in SG), S = SG * tanh(c)
+__global__ void k_tr_sent(float* __restrict__ SG, const float* __restrict__ Cs, float* __restrict__ S, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float sg = sigmoidf_(SG[i]);
+  SG[i] = sg;
+  S[i] = sg * tanhf(Cs[i]);
+}
+
+// copy columns [c0, c0 + n) of a row matrix
+__global__ void k_copy_cols(const float* __restrict__ src, int64_t lds, int c0, float* __restrict__ dst, int64_t ldd,
+                            int rows, int n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * n) return;
+  const int r = (int)(i / n), c = (int)(i % n);
+  dst[(int64_t)r * ldd + c] = src[(int64_t)r * lds + c0 + c];
+}
+
+// Atten.forward for one (t, b) row (adaptive_attention.py:34-56), projections precomputed:
+// PG = W_g h_t, PS = W_s s_t (row pitch PP), VWv[b] = W_v V_b.  Writes alpha (pitch PP), beta,
+// the context c_t and u = c_hat + h_t (the mlp input, :132).  256 threads.
+__global__ __launch_bounds__(256) void k_tr_atten(int B, int H, const float* __restrict__ PG, const float* __restrict__ PS,
+                                                  const float* __restrict__ VWv, const float* __restrict__ Vf,
+                                                  const float* __restrict__ wh, const float* __restrict__ Hs,
+                                                  const float* __restrict__ S, float* __restrict__ alpha,
+                                                  float* __restrict__ beta, float* __restrict__ ctx,
+                                                  float* __restrict__ U) {
+  __shared__ float zs[PP], al[PP], sh_b;
+  const int r = blockIdx.x, b = r % B, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float* pg = PG + (int64_t)r * PP;
+  // scores z_k = w_h . tanh(VWv[b][k] + PG), k < 49; z_s = w_h . tanh(PS + PG): one wave per item
+  for (int k = w; k <= P; k += 4) {
+    float z = 0.f;
+    if (lane < P) {
+      const float x = (k < P ? VWv[((int64_t)b * P + k) * PP + lane] : PS[(int64_t)r * PP + lane]) + pg[lane];
+      z = wh[lane] * tanhf(x);
+    }
+    z = wave_sum(z);
+    if (lane == 0) zs[k] = z;
+  }
+  __syncthreads();
+  if (w == 0) {  // softmax_49 (alpha), softmax_50 (beta = its last entry)
+    const float z = lane < P ? zs[lane] : -INFINITY;
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float a = e / wave_sum(e);
+    if (lane < P) {
+      al[lane] = a;
+      alpha[(int64_t)r * PP + lane] = a;
+    }
+    const float zsn = zs[P];
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      sh_b = es / S2;
+      beta[r] = es / S2;
+    }
+  }
+  __syncthreads();
+  const float be = sh_b;
+  const float* vb = Vf + (int64_t)b * P * H;
+  for (int d = t; d < H; d += 256) {
+    float c = 0.f;
+    for (int k = 0; k < P; ++k) c = __builtin_fmaf(al[k], vb[(int64_t)k * H + d], c);
+    ctx[(int64_t)r * H + d] = c;
+    const float chat = be * S[(int64_t)r * H + d] + (1.f - be) * c;
+    U[(int64_t)r * H + d] = chat + Hs[(int64_t)r * H + d];
+  }
+}
+
+// packed row map: prow[p] = t B + b for the rows of pack_padded_sequence (lengths sorted desc)
+__global__ void k_tr_prow(const int* __restrict__ len, int B, int T, int* __restrict__ prow) {
+  // one thread per (t, b); batch size of t = #{b : len[b] > t}; offset = sum of earlier sizes
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T) return;
+  const int t = i / B, b = i % B;
+  if (len[b] <= t) return;
+  int off = 0;
+  for (int tt = 0; tt < t; ++tt) {
+    int lo = 0, hi = B;  // first b with len[b] <= tt
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (len[mid] > tt) lo = mid + 1;
+      else hi = mid;
+    }
+    off += lo;
+  }
+  prow[off + b] = t * B + b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward pieces
+// ---------------------------------------------------------------------------------------------
+// Atten backward, one workgroup per image b over its steps t < len[b] in order (rows t >= len[b]
+// carry no loss gradient), 256 threads, HPT = H / 256 columns per thread.
+// In: dU (= dc_hat; u = c_hat + h also gives dh = dU directly), alpha, beta, ctx (c_t), S, PG,
+// PS, VWv, V, w_h.  Out per row: dS = beta dU, dPG, dPS (pitch PP); per image: dV[b] (+)= sum_t
+// alpha_t (x) dc_t, dVWv[b] = sum_t dcontent_v, dwh_part[b][j].
+//   beta = softmax_50([z; z_s])[49]:  dz_k += -dbeta beta (1 - beta) alpha_k, dz_s = dbeta beta (1 - beta)
+//   alpha = softmax_49(z):           dz_k += alpha_k (dalpha_k - <alpha, dalpha>)
+template <int HPT>
+__global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restrict__ len, const float* __restrict__ dU,
+                                                      const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                      const float* __restrict__ ctx, const float* __restrict__ S,
+                                                      const float* __restrict__ PG, const float* __restrict__ PS,
+                                                      const float* __restrict__ VWv, const float* __restrict__ Vf,
+                                                      const float* __restrict__ wh, float* __restrict__ dS,
+                                                      float* __restrict__ dPG, float* __restrict__ dPS,
+                                                      float* __restrict__ dV, float* __restrict__ dVWv,
+                                                      float* __restrict__ dwh_part) {
+  constexpr int H = 256 * HPT;
+  __shared__ float s_al[PP], s_da[PP], s_dz[PP], s_red[4], s_dzs;
+  __shared__ float s_dc[H];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float* vb = Vf + (int64_t)b * P * H;
+  float dv_acc[HPT][P];
+#pragma unroll
+  for (int i = 0; i < HPT; ++i)
+#pragma unroll
+    for (int k = 0; k < P; ++k) dv_acc[i][k] = 0.f;
+  float dvwv_acc[P];  // thread j < 49 owns column j of dVWv[b]
+#pragma unroll
+  for (int k = 0; k < P; ++k) dvwv_acc[k] = 0.f;
+  float dwh_acc = 0.f;
+  const float whj = t < P ? wh[t] : 0.f;
+  const int nt = len[b];
+  for (int tt = 0; tt < nt; ++tt) {
+    const int r = tt * B + b;
+    const float be = beta[r];
+    float part = 0.f;
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) {
+      const int d = t + 256 * i;
+      const float du = dU[(int64_t)r * H + d];
+      part += du * (S[(int64_t)r * H + d] - ctx[(int64_t)r * H + d]);
+      dS[(int64_t)r * H + d] = be * du;
+      s_dc[d] = (1.f - be) * du;
+    }
+    part = wave_sum(part);
+    if (lane == 0) s_red[w] = part;
+    if (t < PP) s_al[t] = t < P ? alpha[(int64_t)r * PP + t] : 0.f;
+    __syncthreads();
+    const float dbeta = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    for (int k = w; k < P; k += 4) {  // dalpha_k = dc . V_k
+      float a = 0.f;
+      for (int d = lane; d < H; d += 64) a = __builtin_fmaf(s_dc[d], vb[(int64_t)k * H + d], a);
+      a = wave_sum(a);
+      if (lane == 0) s_da[k] = a;
+    }
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) {  // dV[b][k][d] += alpha_k dc_d
+      const float dcd = s_dc[t + 256 * i];
+#pragma unroll
+      for (int k = 0; k < P; ++k) dv_acc[i][k] = __builtin_fmaf(s_al[k], dcd, dv_acc[i][k]);
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float a = lane < P ? s_al[lane] : 0.f;
+      const float da = lane < P ? s_da[lane] : 0.f;
+      const float dot = wave_sum(a * da);
+      const float dzb = dbeta * be * (1.f - be);
+      if (lane < P) s_dz[lane] = a * (da - dot) - dzb * a;
+      if (lane == 0) s_dzs = dzb;
+    }
+    __syncthreads();
+    if (t < P) {  // thread j: content_v[k][j] for all k, content_s[j]
+      const int j = t;
+      const float pgj = PG[(int64_t)r * PP + j];
+      float sdcv = 0.f, sdw = 0.f;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const float th = tanhf(VWv[((int64_t)b * P + k) * PP + j] + pgj);
+        const float dcv = s_dz[k] * whj * (1.f - th * th);
+        dvwv_acc[k] += dcv;
+        sdcv += dcv;
+        sdw = __builtin_fmaf(s_dz[k], th, sdw);
+      }
+      const float ths = tanhf(PS[(int64_t)r * PP + j] + pgj);
+      const float dcs = s_dzs * whj * (1.f - ths * ths);
+      dPS[(int64_t)r * PP + j] = dcs;
+      dPG[(int64_t)r * PP + j] = sdcv + dcs;
+      dwh_acc += sdw + s_dzs * ths;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int d = t + 256 * i;
+#pragma unroll
+    for (int k = 0; k < P; ++k) dV[((int64_t)b * P + k) * H + d] = dv_acc[i][k];
+  }
+  if (t < P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) dVWv[((int64_t)b * P + k) * PP + t] = dvwv_acc[k];
+    dwh_part[(int64_t)b * PP + t] = dwh_acc;
+  }
+}
+
+// gather rows: dst[i] = src[rows[i]]
+__global__ void k_gather_rows(const float* __restrict__ src, const int* __restrict__ rows, int n, int cols,
+                              float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * cols) return;
+  const int r = (int)(i / cols), c = (int)(i % cols);
+  dst[i] = src[(int64_t)rows[r] * cols + c];
+}
+
+// sentinel backward: s = SG * tanh(c): dG = dS tanh(c) SG (1 - SG); dC += dS SG (1 - tanh(c)^2)
+__global__ void k_tr_sent_bwd(const float* __restrict__ dS, const float* __restrict__ SG, const float* __restrict__ Cs,
+                              float* __restrict__ dG, float* __restrict__ dC, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float sg = SG[i], tc = tanhf(Cs[i]), ds = dS[i];
+  dG[i] = ds * tc * sg * (1.f - sg);
+  dC[i] = ds * sg * (1.f - tc * tc);
+}
+
+// LSTM cell backward of step t (rows b < B): dh = dH[t] + dh_rec, dc = dC[t] + dc_rec;
+// writes DG[t] (pre-activation gate grads) and dc_rec <- dc * f
+__global__ void k_tr_cell_bwd(const float* __restrict__ dH, const float* __restrict__ dC, const float* __restrict__ dh_rec,
+                              float* __restrict__ dc_rec, const float* __restrict__ GA, const float* __restrict__ c_t,
+                              const float* __restrict__ c_prev, int B, int H, float* __restrict__ DG) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * H) return;
+  const int b = (int)(i / H), j = (int)(i % H);
+  const float* ga = GA + (int64_t)b * 4 * H;
+  const float i_ = ga[j], f_ = ga[H + j], g_ = ga[2 * H + j], o_ = ga[3 * H + j];
+  const float c = c_t[i], tc = tanhf(c);
+  const float dh = dH[i] + dh_rec[i];
+  float dc = dC[i] + dc_rec[i] + dh * o_ * (1.f - tc * tc);
+  const float d_o = dh * tc;
+  const float d_i = dc * g_, d_g = dc * i_, d_f = dc * c_prev[i];
+  float* dg = DG + (int64_t)b * 4 * H;
+  dg[j] = d_i * i_ * (1.f - i_);
+  dg[H + j] = d_f * f_ * (1.f - f_);
+  dg[2 * H + j] = d_g * (1.f - g_ * g_);
+  dg[3 * H + j] = d_o * o_ * (1.f - o_);
+  dc_rec[i] = dc * f_;
+}
+
+// embedding gradient: dE[v] = sum over (t, b) with tok == v of dX[t B + b][0:E], in (t, b) order
+__global__ void k_tr_embed_bwd(const int64_t* __restrict__ tok, int tld, const int* __restrict__ len, int B, int T,
+                               const float* __restrict__ dX, int E, int V, float* __restrict__ dE) {
+  const int v = blockIdx.x;
+  if (v >= V) return;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < T; ++t)
+      for (int b = 0; b < B; ++b) {
+        int64_t tk = tok[(int64_t)b * tld + t];
+        tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+        if (tk == v) s += dX[((int64_t)t * B + b) * 2 * E + e];
+      }
+    dE[(int64_t)v * E + e] = s;
+  }
+  (void)len;
+}
+
+// dv_g[b] = sum_t dX[t B + b][E:2E] (in t order), then relu'(v_g)
+__global__ void k_tr_vg_bwd(const float* __restrict__ dX, const float* __restrict__ vg, int B, int T, int E,
+                            float* __restrict__ dvg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * E) return;
+  const int b = (int)(i / E), e = (int)(i % E);
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) s += dX[((int64_t)t * B + b) * 2 * E + E + e];
+  dvg[i] = vg[i] > 0.f ? s : 0.f;
+}
+
+// elementwise helpers
+__global__ void k_relu_mask(float* __restrict__ d, const float* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !(y[i] > 0.f)) d[i] = 0.f;
+}
+__global__ void k_tanh_bwd(float* __restrict__ d, const float* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = d[i] * (1.f - y[i] * y[i]);
+}
+__global__ void k_rowsum_pp(const float* __restrict__ X, int rows, float* __restrict__ out) {  // [rows][PP] -> [P]
+  const int j = threadIdx.x;
+  if (j >= P) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += X[(int64_t)r * PP + j];
+  out[j] = s;
+}
+
+}  // namespace aa
+
+// ---------------------------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------------------------
+struct TrainWS {
+  float *a_g, *V, *vg, *h0, *c0, *VWv, *X, *PRE, *G4, *GA, *Hs, *Cs, *SG, *S, *PG, *PS, *alpha, *beta, *ctx, *U;
+  int* prow;
+  // backward scratch
+  float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg;
+};
+
+static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax, size_t* bytes) {
+  Carver c{base};
+  const size_t H = d.hidden, E = d.embed, Cc = d.channels, R = (size_t)T * B, P_ = aa::P, PP_ = aa::PP;
+  TrainWS w;
+  w.a_g = c.take<float>(B * Cc);
+  w.V = c.take<float>(B * P_ * H);
+  w.vg = c.take<float>(B * E);
+  w.h0 = c.take<float>(B * H);
+  w.c0 = c.take<float>(B * H);
+  w.VWv = c.take<float>(B * P_ * PP_);
+  w.X = c.take<float>(R * 2 * E);
+  w.PRE = c.take<float>(R * 5 * H);
+  w.G4 = c.take<float>(B * 4 * H);
+  w.GA = c.take<float>(R * 4 * H);
+  w.Hs = c.take<float>(R * H);
+  w.Cs = c.take<float>(R * H);
+  w.SG = c.take<float>(R * H);
+  w.S = c.take<float>(R * H);
+  w.PG = c.take<float>(R * PP_);
+  w.PS = c.take<float>(R * PP_);
+  w.alpha = c.take<float>(R * PP_);
+  w.beta = c.take<float>(R);
+  w.ctx = c.take<float>(R * H);
+  w.U = c.take<float>(R * H);
+  w.prow = c.take<int>(R);
+  w.Up = c.take<float>((size_t)Nmax * H);
+  w.dU = c.take<float>(R * H);
+  w.dS = c.take<float>(R * H);
+  w.dPG = c.take<float>(R * PP_);
+  w.dPS = c.take<float>(R * PP_);
+  w.dV = c.take<float>(B * P_ * H);
+  w.dVWv = c.take<float>(B * P_ * PP_);
+  w.dwh = c.take<float>(B * PP_);
+  w.dH = c.take<float>(R * H);
+  w.dC = c.take<float>(R * H);
+  w.dG = c.take<float>(R * H);
+  w.DG = c.take<float>(R * 4 * H);
+  w.dX = c.take<float>(R * 2 * E);
+  w.dh_rec = c.take<float>(B * H);
+  w.dc_rec = c.take<float>(B * H);
+  w.dvg = c.take<float>(B * E);
+  *bytes = c.off;
+  return w;
+}
+
+static int train_check(const aa_dims* d, int B, int T) {
+  if (!d) return AA_ERR_NULL;
+  if (aa_check_dims(d) != AA_OK) return AA_ERR_DIMS;
+  if (B < 0 || T < 0) return AA_ERR_SHAPE;
+  if (2 * d->embed > 4096) return AA_ERR_DIMS;
+  return AA_OK;
+}
+
+size_t aa_train_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
+  if (train_check(d, B, T) != AA_OK) return 0;
+  size_t n;
+  carve_train(nullptr, *d, B, T, B * T, &n);
+  return n;
+}
+
+static inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
+                     const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, float* scores, int32_t N,
+                     void* workspace, size_t workspace_bytes, aa_stream_t stream) {
+  using namespace aa;
+  int rc = train_check(dims, B, T);
+  if (rc) return rc;
+  if (B == 0 || T == 0 || N == 0) return AA_OK;
+  if (!w || !feats || !tokens || !lengths || !scores || !workspace || !w->sent_affine_h_w) return AA_ERR_NULL;
+  if (N > B * T || tok_ld < T) return AA_ERR_SHAPE;
+  size_t need;
+  TrainWS s = carve_train(static_cast<char*>(workspace), *dims, B, T, B * T, &need);
+  if (workspace_bytes < need) return AA_ERR_BUFFER;
+  const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B;
+  hipStream_t st = (hipStream_t)stream;
+  // encoder tail (baseline_attention.py:46-60), reference weight layouts
+  hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
+  {
+    const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
+    hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, st, feats, B, C, H, w->enc_affine_a_w,
+                       w->enc_affine_a_b, s.V);
+  }
+  tgemm(st, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
+  tgemm(st, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
+  tgemm(st, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
+  tgemm(st, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
+  // x_t and the step-invariant input terms for all steps
+  hipLaunchKernelGGL(k_tr_x, dim3(R), dim3(256), 0, st, tokens, tok_ld, w->embed_w, V, E, s.vg, B, T, s.X);
+  tgemm(st, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
+  tgemm(st, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
+  // LSTM over T steps (baseline_attention.py:167-178)
+  for (int t = 0; t < T; ++t) {
+    const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
+    const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
+    tgemm(st, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
+    hipLaunchKernelGGL(k_tr_cell, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.G4, s.PRE + (size_t)t * B * 5 * H,
+                       5 * H, cp, B, H, s.Hs + (size_t)t * B * H, s.Cs + (size_t)t * B * H,
+                       s.GA + (size_t)t * B * 4 * H);
+  }
+  // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
+  hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
+                     (int64_t)H, R, H);
+  tgemm(st, R - B, H, H, s.Hs, H, 0, w->sent_affine_h_w, H, 0, s.SG + (size_t)B * H, H, 1);
+  hipLaunchKernelGGL(k_tr_sent, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.SG, s.Cs, s.S, (int64_t)R * H);
+  // attention projections and the attention itself (adaptive_attention.py:26-58)
+  tgemm(st, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
+  tgemm(st, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
+  hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs, s.S,
+                     s.alpha, s.beta, s.ctx, s.U);
+  // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
+  hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
+  tgemm(st, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
+  return aa_launch_status();
+}
+
+int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
+                      const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, const float* dscores, int32_t N,
+                      const aa_ref_grads* grads, void* workspace, size_t workspace_bytes, aa_stream_t stream) {
+  using namespace aa;
+  int rc = train_check(dims, B, T);
+  if (rc) return rc;
+  if (B == 0 || T == 0 || N == 0) return AA_OK;
+  if (!w || !feats || !tokens || !lengths || !dscores || !grads || !workspace) return AA_ERR_NULL;
+  if (N > B * T || tok_ld < T) return AA_ERR_SHAPE;
+  size_t need;
+  TrainWS s = carve_train(static_cast<char*>(workspace), *dims, B, T, B * T, &need);
+  if (workspace_bytes < need) return AA_ERR_BUFFER;
+  const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B, E2 = 2 * E;
+  hipStream_t st = (hipStream_t)stream;
+#define GRAD(f) (grads->f)
+  const size_t RH = (size_t)R * H;
+  // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)
+  AA_TRY(hipMemsetAsync(s.dU, 0, sizeof(float) * RH, st));
+  tgemm(st, N, H, V, dscores, V, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
+  hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
+  tgemm(st, V, H, N, dscores, V, 1, s.Up, H, 1, GRAD(mlp_w), H);
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(V)), dim3(256), 0, st, dscores, N, V, (int64_t)V, GRAD(mlp_b), 0);
+  // Atten backward (adaptive_attention.py:26-58)
+  AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
+  AA_TRY(hipMemsetAsync(s.dPG, 0, sizeof(float) * (size_t)R * PP, st));
+  AA_TRY(hipMemsetAsync(s.dPS, 0, sizeof(float) * (size_t)R * PP, st));
+#define AA_ATB(HPT_)                                                                                          \
+  hipLaunchKernelGGL(k_tr_atten_bwd<HPT_>, dim3(B), dim3(256), 0, st, B, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, \
+                     s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, s.dV, s.dVWv, s.dwh)
+  switch (H / 256) {
+    case 1: AA_ATB(1); break;
+    case 2: AA_ATB(2); break;
+    case 3: AA_ATB(3); break;
+    default: AA_ATB(4); break;
+  }
+#undef AA_ATB
+  AA_TRY(hipMemcpyAsync(s.dH, s.dU, sizeof(float) * RH, hipMemcpyDeviceToDevice, st));  // u = c_hat + h
+  tgemm(st, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
+  tgemm(st, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
+  tgemm(st, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
+  tgemm(st, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
+  tgemm(st, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
+  tgemm(st, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
+  hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(64), 0, st, s.dwh, B, GRAD(att_affine_h_w));
+  // Sentinel backward (:79-83): h_{t-1} input = Hs[r - B] for r >= B, 0 for t = 0
+  hipLaunchKernelGGL(k_tr_sent_bwd, dim3(nblk((int64_t)RH)), dim3(256), 0, st, s.dS, s.SG, s.Cs, s.dG, s.dC,
+                     (int64_t)RH);
+  tgemm(st, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
+  tgemm(st, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
+  tgemm(st, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
+  tgemm(st, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
+  // LSTM backward through time (baseline_attention.py:167-178)
+  AA_TRY(hipMemsetAsync(s.dh_rec, 0, sizeof(float) * (size_t)B * H, st));
+  AA_TRY(hipMemsetAsync(s.dc_rec, 0, sizeof(float) * (size_t)B * H, st));
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t o = (size_t)t * B * H;
+    const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
+    hipLaunchKernelGGL(k_tr_cell_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o, s.dh_rec,
+                       s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H, s.DG + (size_t)t * B * 4 * H);
+    tgemm(st, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);  // dh_{t-1}
+  }
+  tgemm(st, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
+  tgemm(st, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);
+  tgemm(st, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(4 * H)), dim3(256), 0, st, s.DG, R, 4 * H, (int64_t)4 * H, GRAD(lstm_b_ih), 0);
+  AA_TRY(hipMemcpyAsync(GRAD(lstm_b_hh), GRAD(lstm_b_ih), sizeof(float) * 4 * H, hipMemcpyDeviceToDevice, st));
+  tgemm(st, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
+  // x_t = [embed(tok); v_g] (baseline_attention.py:151-154)
+  hipLaunchKernelGGL(k_tr_embed_bwd, dim3(V), dim3(256), 0, st, tokens, tok_ld, lengths, B, T, s.dX, E, V,
+                     GRAD(embed_w));
+  hipLaunchKernelGGL(k_tr_vg_bwd, dim3(nblk((int64_t)B * E)), dim3(256), 0, st, s.dX, s.vg, B, T, E, s.dvg);
+  // encoder tail (baseline_attention.py:46-60)
+  tgemm(st, E, C, B, s.dvg, E, 1, s.a_g, C, 1, GRAD(enc_affine_b_w), C);
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(E)), dim3(256), 0, st, s.dvg, B, E, (int64_t)E, GRAD(enc_affine_b_b), 0);
+  hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)B * H);
+  hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dc_rec, s.c0, (int64_t)B * H);
+  tgemm(st, H, C, B, s.dh_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_h0_w), C);
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dh_rec, B, H, (int64_t)H, GRAD(enc_affine_h0_b), 0);
+  tgemm(st, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dc_rec, B, H, (int64_t)H, GRAD(enc_affine_c0_b), 0);
+  hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, st, s.dV, s.V, (int64_t)B * P * H);
+  tgemm(st, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);                // dW_a = dV^T A
+  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dV, B * P, H, (int64_t)H, GRAD(enc_affine_a_b), 0);
+#undef GRAD
+  return aa_launch_status();
+}

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 4
+#define AA_ABI_VERSION 5
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -82,6 +82,31 @@ typedef struct aa_ref_weights {
   const float* mlp_w;           /* decoder.adaptive.mlp.weight [V, H] */
   const float* mlp_b;           /* decoder.adaptive.mlp.bias   [V]    */
 } aa_ref_weights;
+
+/* Gradient outputs of aa_train_backward, same fields and shapes as aa_ref_weights. */
+typedef struct aa_ref_grads {
+  float* enc_affine_a_w;
+  float* enc_affine_a_b;
+  float* enc_affine_b_w;
+  float* enc_affine_b_b;
+  float* enc_affine_h0_w;
+  float* enc_affine_h0_b;
+  float* enc_affine_c0_w;
+  float* enc_affine_c0_b;
+  float* embed_w;
+  float* lstm_w_ih;
+  float* lstm_w_hh;
+  float* lstm_b_ih;
+  float* lstm_b_hh;
+  float* sent_affine_x_w;
+  float* sent_affine_h_w;
+  float* att_affine_v_w;
+  float* att_affine_g_w;
+  float* att_affine_s_w;
+  float* att_affine_h_w;
+  float* mlp_w;
+  float* mlp_b;
+} aa_ref_grads;
 
 /* A model = dims + a caller-owned device buffer holding the packed (kernel-layout) weights. */
 typedef struct aa_model {
@@ -188,6 +213,27 @@ AA_API int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t 
                                  aa_decode_plan** plan);
 AA_API int aa_decode_plan_launch(const aa_decode_plan* plan, aa_stream_t stream);
 AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
+
+/* ---- teacher-forced training step ----------------------------------------
+ * Encoder2Decoder.forward(images, captions, lengths) (baseline_attention.py:206-230) and its
+ * backward, fp32, deterministic.  feats [B,C,7,7]; tokens: captions [B][tok_ld] int64 (column t is
+ * the input token of step t, <start> first); lengths: DEVICE int32 [B], sorted descending (as
+ * pack_padded_sequence requires), T = lengths[0] steps, N = sum(lengths) packed rows.
+ * aa_train_forward writes the packed scores [N][V] (pack_padded_sequence(scores, lengths).data:
+ * rows t-major over the batch entries still running at step t) and keeps the activations in the
+ * workspace; aa_train_backward takes dL/dscores [N][V] with the same arguments and workspace and
+ * writes the gradient of every parameter (assigned, not accumulated).  The reference's loss
+ * (train.py: CrossEntropyLoss on the packed scores) stays with the caller. */
+AA_API size_t aa_train_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
+AA_API int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B,
+                            int32_t T, const int64_t* tokens, int32_t tok_ld, const int32_t* lengths,
+                            float* scores, int32_t N, void* workspace, size_t workspace_bytes,
+                            aa_stream_t stream);
+AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats,
+                             int32_t B, int32_t T, const int64_t* tokens, int32_t tok_ld,
+                             const int32_t* lengths, const float* dscores, int32_t N,
+                             const aa_ref_grads* grads, void* workspace, size_t workspace_bytes,
+                             aa_stream_t stream);
 
 /* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
  * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */

@@ -144,3 +144,36 @@ def sampler(state: Dict[str, np.ndarray], feats: np.ndarray, max_len: int = 20, 
     """numpy in / torch out convenience wrapper."""
     m = OracleModel(state)
     return m.sampler(torch.from_numpy(np.ascontiguousarray(feats)), max_len=max_len, keep_scores=keep_scores)
+
+
+class TrainOracle(OracleModel):
+    """Teacher-forced ``Encoder2Decoder.forward`` (``baseline_attention.py:206-230``) with autograd:
+    every reference parameter is a leaf tensor with ``requires_grad`` (``self.w``), the LSTM is an
+    ``nn.LSTM`` whose parameters are those leaves.  D2 is moot here: the states
+    are transposed out of place.  Returns the packed scores like ``pack_padded_sequence``."""
+
+    def __init__(self, state: Dict[str, np.ndarray]):
+        super().__init__(state)
+        for v in self.w.values():
+            v.requires_grad_(True)
+        self.lstm.train()
+        self.lstm.requires_grad_(True)
+        with torch.no_grad():  # the LSTM module's own parameters ARE the leaves of self.w
+            for n in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0"):
+                setattr(self.lstm, n, torch.nn.Parameter(self.w["decoder.LSTM." + n]))
+        for n in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0"):
+            self.w["decoder.LSTM." + n] = getattr(self.lstm, n)
+        self.lstm.flatten_parameters()
+
+    def forward(self, images: torch.Tensor, captions: torch.Tensor, lengths):
+        from torch.nn.utils.rnn import pack_padded_sequence
+        V, v_g, states, _ = self.encoder(images)                                    # :213-219
+        scores, _, _, _ = self.decoder(V, v_g, captions, states)                      # :225
+        return pack_padded_sequence(scores, list(lengths), batch_first=True)        # :228
+
+    def loss(self, images, captions, lengths):
+        """train.py:101,204-208: CE over the packed scores against the packed next tokens."""
+        from torch.nn.utils.rnn import pack_padded_sequence
+        packed = self.forward(images, captions, lengths)
+        targets = pack_padded_sequence(captions[:, 1:], list(lengths), batch_first=True)[0]
+        return torch.nn.functional.cross_entropy(packed[0], targets), packed

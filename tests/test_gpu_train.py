@@ -1,0 +1,127 @@
+"""Teacher-forced training step (Encoder2Decoder.forward + backward) on the GPU,
+through the C-ABI (aa_train_forward / aa_train_backward), against the REAL reference's forward,
+loss and gradients (tests/golden/train_b4.npz, made by tests/golden/make_golden_train.py) and
+against the autograd of the CPU oracle on ragged batches.
+
+Tolerances: the GPU path is fp32 with a different summation order than the reference's CPU
+kernels, so packed scores agree to 1e-4 absolute, the loss to 1e-5 relative, and each gradient to
+1e-3 relative (Frobenius) with every entry within 1e-2 of that parameter's largest gradient
+magnitude.  (Entry-wise agreement is not tighter because a ReLU input within rounding of 0 can
+take the other side of the kink: affine_a / affine_b gradients then differ in one row.)"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+from torch.nn.utils.rnn import pack_padded_sequence
+
+from conftest import load_golden
+
+from adaptive_amd import Config, Encoder2Decoder, synth
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL = 1e-4
+GRAD_REL = 1e-3    # relative Frobenius error per parameter
+GRAD_ENTRY = 1e-2  # max entry error / max |gradient|
+
+
+def _grad_close(got, ref, name):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    assert np.abs(got - ref).max() <= GRAD_ENTRY * scale, name
+    assert np.linalg.norm(got - ref) <= GRAD_REL * max(np.linalg.norm(ref), 1e-30), name
+
+
+def _model(dev, seed=123, noise=0.02):
+    return Encoder2Decoder(Config()).to(dev).load_synthetic(seed, bias_noise=noise)
+
+
+def _loss(model, feats, caps, lengths):
+    packed = model(feats, caps, lengths)
+    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]
+    return F.cross_entropy(packed[0], targets), packed
+
+
+def test_train_step_vs_reference_golden(gpu_device):
+    g = load_golden("train_b4")
+    model = _model(gpu_device)
+    feats = torch.from_numpy(synth.make_features(4, seed=7)).to(gpu_device)
+    caps = torch.from_numpy(g["captions"]).to(gpu_device)
+    lengths = g["lengths"].tolist()
+    loss, packed = _loss(model, feats, caps, lengths)
+    assert packed[1].tolist() == g["batch_sizes"].tolist()
+    np.testing.assert_allclose(packed[0].detach().cpu().numpy(), g["scores"], atol=SCORE_TOL, rtol=0)
+    assert abs(loss.item() - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+    model.zero_grad()
+    loss.backward()
+    for k, p in model.named_parameters():
+        got = p.grad.detach().cpu().numpy().reshape(-1)
+        ref = g["g:" + k]
+        if "g:" + k + ":idx" in g:
+            got_s = got[g["g:" + k + ":idx"]]
+        else:
+            got_s = got
+        _grad_close(got_s, ref, k)
+        ref_norm = float(g["g:" + k + ":norm"])
+        assert abs(np.linalg.norm(got.astype(np.float64)) - ref_norm) <= 1e-4 * max(ref_norm, 1e-12), k
+
+
+def test_train_step_vs_oracle_ragged(gpu_device):
+    """B = 13, lengths with ties and a length-1 row, captions wider than T + 1."""
+    from oracle.adaptive_oracle import TrainOracle
+    B, L = 13, 12
+    lengths = [9, 9, 8, 7, 7, 6, 5, 4, 4, 3, 2, 1, 1]
+    rng = np.random.default_rng(5)
+    caps_np = rng.integers(0, 10123, size=(B, L)).astype(np.int64)
+    caps_np[:, 0] = 1
+    state = synth.make_weights(31, bias_noise=0.01)
+    feats_np = synth.make_features(B, seed=9)
+    oracle = TrainOracle(state)
+    rloss, rpacked = oracle.loss(torch.from_numpy(feats_np), torch.from_numpy(caps_np), lengths)
+    rloss.backward()
+    model = _model(gpu_device, seed=31, noise=0.01)
+    loss, packed = _loss(model, torch.from_numpy(feats_np).to(gpu_device), torch.from_numpy(caps_np).to(gpu_device),
+                         lengths)
+    np.testing.assert_allclose(packed[0].detach().cpu().numpy(), rpacked[0].detach().numpy(), atol=SCORE_TOL, rtol=0)
+    assert abs(loss.item() - rloss.item()) <= 1e-5 * abs(rloss.item())
+    loss.backward()
+    for k, p in model.named_parameters():
+        got = p.grad.detach().cpu().numpy()
+        _grad_close(got, oracle.w[k].grad.detach().numpy(), k)
+
+
+def test_train_step_deterministic(gpu_device):
+    g = load_golden("train_b4")
+    feats = torch.from_numpy(synth.make_features(4, seed=7)).to(gpu_device)
+    caps = torch.from_numpy(g["captions"]).to(gpu_device)
+    grads = []
+    for _ in range(2):
+        model = _model(gpu_device)
+        loss, _ = _loss(model, feats, caps, g["lengths"].tolist())
+        loss.backward()
+        grads.append({k: p.grad.clone() for k, p in model.named_parameters()})
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+def test_train_closure_adam_clip_reduces_loss(gpu_device):
+    """train.py:197-219 as written: zero_grad, forward, CE, backward, clip LSTM grad norm, Adam step."""
+    B, L = 8, 10
+    lengths = [9, 8, 8, 6, 5, 5, 3, 2]
+    rng = np.random.default_rng(11)
+    caps = torch.from_numpy(rng.integers(0, 10123, size=(B, L)).astype(np.int64)).to(gpu_device)
+    caps[:, 0] = 1
+    feats = torch.from_numpy(synth.make_features(B, seed=3)).to(gpu_device)
+    model = _model(gpu_device)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(5):
+        model.zero_grad()
+        opt.zero_grad()
+        loss, _ = _loss(model, feats, caps, lengths)
+        losses.append(loss.item())
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+        opt.step()
+    assert losses[-1] < losses[0]

@@ -46,6 +46,6 @@ def test_cpu_tensors_are_rejected(model):
         model.sampler(torch.zeros(2, 2048, 7, 7))
 
 
-def test_teacher_forcing_not_silently_faked(model):
-    with pytest.raises(NotImplementedError):
-        model(torch.zeros(2, 2048, 7, 7), torch.zeros(2, 5, dtype=torch.long), [5, 4])
+def test_teacher_forcing_has_no_cpu_path(model):
+    with pytest.raises(RuntimeError, match="GPU|CUDA"):
+        model(torch.zeros(2, 2048, 7, 7), torch.zeros(2, 5, dtype=torch.long), [4, 3])
