@@ -42,53 +42,80 @@ struct TG {
   const float* bias;
   const float* bias2;
   int accumulate;
-  int act;  // 0 none, 1 relu, 2 tanh
+  int act;      // 0 none, 1 relu, 2 tanh
+  int splits;   // split-K: > 1 -> raw partial tiles to part[split][M][N], reduced by k_tgemm_reduce
+  int kper;     // K per split (multiple of BK)
+  float* part;
 };
 
 __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][64 * LDK];
   const int tilesN = (g.N + 63) / 64;
-  const int mt = blockIdx.x / tilesN, nt = blockIdx.x % tilesN;
+  const int split = blockIdx.x % g.splits, tile = blockIdx.x / g.splits;
+  const int mt = tile / tilesN, nt = tile % tilesN;
+  const int kbeg = split * g.kper, kend = g.splits > 1 ? (kbeg + g.kper < g.K ? kbeg + g.kper : g.K) : g.K;
   const int m0 = mt * 64, n0 = nt * 64;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wmv = wave >> 1, wnv = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
   float ra[8], rw[8];
+  // operands are read 8 consecutive elements per thread along their contiguous dimension, as two
+  // 16-B loads when the 8 are in bounds and aligned, else element by element with zero fill
+  const bool a4 = ((g.lda & 3) == 0) && ((((uintptr_t)g.A) & 15) == 0);
+  const bool w4 = ((g.ldw & 3) == 0) && ((((uintptr_t)g.W) & 15) == 0) && g.wm != 2;
+  auto load8 = [&](float (&r)[8], const float* base, bool fast) {
+    if (fast) {
+      const float4 x = *reinterpret_cast<const float4*>(base), y = *reinterpret_cast<const float4*>(base + 4);
+      r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w; r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+    }
+  };
   auto gload = [&](int k0) {
     if (!g.at) {  // 4 threads per row, 8 consecutive k each
       const int r = t >> 2, kq = (t & 3) * 8, m = m0 + r;
       const int64_t base = (int64_t)(m < g.M ? (g.arow ? g.arow[m] : m) : 0) * g.lda;
+      const bool fast = a4 && m < g.M && k0 + kq + 8 <= kend;
+      if (fast) load8(ra, g.A + base + k0 + kq, true);
+      else
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = k0 + kq + i;
-        ra[i] = (m < g.M && k < g.K) ? g.A[base + k] : 0.f;
-      }
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + kq + i;
+          ra[i] = (m < g.M && k < kend) ? g.A[base + k] : 0.f;
+        }
     } else {  // 8 threads per k, 8 consecutive m each
       const int k = k0 + (t >> 3), mq = (t & 7) * 8;
+      const bool fast = a4 && k < kend && m0 + mq + 8 <= g.M;
+      if (fast) load8(ra, g.A + (int64_t)k * g.lda + m0 + mq, true);
+      else
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + mq + i;
-        ra[i] = (m < g.M && k < g.K) ? g.A[(int64_t)k * g.lda + m] : 0.f;
-      }
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + mq + i;
+          ra[i] = (m < g.M && k < kend) ? g.A[(int64_t)k * g.lda + m] : 0.f;
+        }
     }
     if (g.wm == 1) {
       const int k = k0 + (t >> 3), nq = (t & 7) * 8;
+      const bool fast = w4 && k < kend && n0 + nq + 8 <= g.N;
+      if (fast) load8(rw, g.W + (int64_t)k * g.ldw + n0 + nq, true);
+      else
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int n = n0 + nq + i;
-        rw[i] = (n < g.N && k < g.K) ? g.W[(int64_t)k * g.ldw + n] : 0.f;
-      }
+        for (int i = 0; i < 8; ++i) {
+          const int n = n0 + nq + i;
+          rw[i] = (n < g.N && k < kend) ? g.W[(int64_t)k * g.ldw + n] : 0.f;
+        }
     } else {
       const int r = t >> 2, kq = (t & 3) * 8, n = n0 + r;
+      const bool fast = w4 && n < g.N && k0 + kq + 8 <= kend;
+      if (fast) load8(rw, g.W + (int64_t)n * g.ldw + k0 + kq, true);
+      else
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = k0 + kq + i;
-        float v = 0.f;
-        if (n < g.N && k < g.K) {
-          if (g.wm == 0) v = g.W[(int64_t)n * g.ldw + k];
-          else v = g.W[((int64_t)(k / P) * g.ldw + n) * P + (k % P)];
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + kq + i;
+          float v = 0.f;
+          if (n < g.N && k < kend) {
+            if (g.wm == 0) v = g.W[(int64_t)n * g.ldw + k];
+            else v = g.W[((int64_t)(k / P) * g.ldw + n) * P + (k % P)];
+          }
+          rw[i] = v;
         }
-        rw[i] = v;
-      }
     }
   };
   auto lstore = [&](int buf) {
@@ -116,13 +143,13 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int nk = (g.K + BK - 1) / BK;
-  gload(0);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  gload(kbeg);
   lstore(0);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nk) gload((ks + 1) * BK);
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * BK);
     const float* As = lds[buf][0];
     const float* Ws = lds[buf][1];
 #pragma unroll
@@ -137,6 +164,15 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   }
   const int col = n0 + wnv * 32 + li;
   if (col >= g.N) return;
+  if (g.splits > 1) {
+    float* pt = g.part + (int64_t)split * g.M * g.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wmv * 32 + acc_row(r, lane);
+      if (m < g.M) pt[(int64_t)m * g.N + col] = acc[r];
+    }
+    return;
+  }
   const float bv = (g.bias ? g.bias[col] : 0.f) + (g.bias2 ? g.bias2[col] : 0.f);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -150,23 +186,78 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   }
 }
 
-// C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites
-static void tgemm(hipStream_t s, int M, int N, int K, const float* A, int64_t lda, int at, const float* W, int64_t ldw,
+// split-K epilogue: partials summed in split order, then bias / act / row map / accumulate
+__global__ void k_tgemm_reduce(TG g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)g.M * g.N) return;
+  const int m = (int)(i / g.N), n = (int)(i % g.N);
+  float v = 0.f;
+  for (int sp = 0; sp < g.splits; ++sp) v += g.part[(int64_t)sp * g.M * g.N + i];
+  v += (g.bias ? g.bias[n] : 0.f) + (g.bias2 ? g.bias2[n] : 0.f);
+  if (g.act == 1) v = reluf_(v);
+  else if (g.act == 2) v = tanhf(v);
+  float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + n;
+  *dst = g.accumulate ? *dst + v : v;
+}
+
+// launch context of a training call: stream + split-K scratch carved from its workspace
+struct GemmCtx {
+  hipStream_t s;
+  float* split;
+  size_t cap;  // floats
+};
+
+// C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites.  GEMMs with
+// too few output tiles to fill the chip are split along K (deterministically reduced).
+static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t lda, int at, const float* W, int64_t ldw,
                   int wm, float* C, int64_t ldc, int accumulate = 0, const float* bias = nullptr,
                   const float* bias2 = nullptr, int act = 0, const int* arow = nullptr, const int* crow = nullptr) {
   if (M <= 0 || N <= 0) return;
-  TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act};
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  hipLaunchKernelGGL(k_tgemm, dim3(tiles), dim3(256), 0, s, g);
+  int splits = 1;
+  const hipStream_t s = gc.s;
+  if (tiles < 128 && K >= 256 && gc.split) {
+    splits = (256 + tiles - 1) / tiles;
+    const int kmax = K / 128;
+    if (splits > kmax) splits = kmax;
+    const size_t capsp = gc.cap / ((size_t)M * N);
+    if ((size_t)splits > capsp) splits = (int)capsp;
+    if (splits < 2) splits = 1;
+  }
+  int kper = K;
+  if (splits > 1) {
+    kper = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+    splits = (K + kper - 1) / kper;
+  }
+  TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, splits, kper,
+       splits > 1 ? gc.split : nullptr};
+  hipLaunchKernelGGL(k_tgemm, dim3(tiles * splits), dim3(256), 0, s, g);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
 }
 
-// column sums: out[n] (+)= sum_m X[m ldx + n] over m in order (deterministic)
-__global__ void k_colsum(const float* __restrict__ X, int M, int N, int64_t ldx, float* __restrict__ out, int accumulate) {
+// column sums: out[n] (+)= sum_m X[m ldx + n], deterministic: rows split into CS_CH fixed chunks
+// summed in order by k_colsum (one thread per (column, chunk)), the chunk sums added in chunk
+// order by k_colsum_fin.
+constexpr int CS_CH = 64;
+__global__ void k_colsum(const float* __restrict__ X, int M, int N, int64_t ldx, float* __restrict__ part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, ch = blockIdx.y;
+  if (n >= N) return;
+  const int per = (M + CS_CH - 1) / CS_CH, m0 = ch * per, m1 = m0 + per < M ? m0 + per : M;
+  float s = 0.f;
+  for (int m = m0; m < m1; ++m) s += X[(int64_t)m * ldx + n];
+  part[(int64_t)ch * N + n] = s;
+}
+__global__ void k_colsum_fin(const float* __restrict__ part, int N, float* __restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float s = 0.f;
-  for (int m = 0; m < M; ++m) s += X[(int64_t)m * ldx + n];
-  out[n] = accumulate ? out[n] + s : s;
+  for (int ch = 0; ch < CS_CH; ++ch) s += part[(int64_t)ch * N + n];
+  out[n] = s;
+}
+static void colsum(hipStream_t st, const float* X, int M, int N, int64_t ldx, float* scratch, float* out) {
+  hipLaunchKernelGGL(k_colsum, dim3((N + 255) / 256, CS_CH), dim3(256), 0, st, X, M, N, ldx, scratch);
+  hipLaunchKernelGGL(k_colsum_fin, dim3((N + 255) / 256), dim3(256), 0, st, scratch, N, out);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -318,6 +409,7 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
   constexpr int H = 256 * HPT;
   __shared__ float s_al[PP], s_da[PP], s_dz[PP], s_red[4], s_dzs;
   __shared__ float s_dc[H];
+  __shared__ float s_cv[P * P], s_tz[P * P];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float* vb = Vf + (int64_t)b * P * H;
   float dv_acc[HPT][P];
@@ -325,9 +417,9 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
   for (int i = 0; i < HPT; ++i)
 #pragma unroll
     for (int k = 0; k < P; ++k) dv_acc[i][k] = 0.f;
-  float dvwv_acc[P];  // thread j < 49 owns column j of dVWv[b]
+  float dvwv_acc[10];  // thread owns entries e = t + 256 i of dVWv[b] (49 x 49)
 #pragma unroll
-  for (int k = 0; k < P; ++k) dvwv_acc[k] = 0.f;
+  for (int i = 0; i < 10; ++i) dvwv_acc[i] = 0.f;
   float dwh_acc = 0.f;
   const float whj = t < P ? wh[t] : 0.f;
   const int nt = len[b];
@@ -370,19 +462,29 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
       if (lane == 0) s_dzs = dzb;
     }
     __syncthreads();
-    if (t < P) {  // thread j: content_v[k][j] for all k, content_s[j]
-      const int j = t;
-      const float pgj = PG[(int64_t)r * PP + j];
-      float sdcv = 0.f, sdw = 0.f;
+    // content_v[k][j] = VWv[b][k][j] + PG[j]: entries e = k * 49 + j spread over the threads
+    const float* pgr = PG + (int64_t)r * PP;
 #pragma unroll
-      for (int k = 0; k < P; ++k) {
-        const float th = tanhf(VWv[((int64_t)b * P + k) * PP + j] + pgj);
-        const float dcv = s_dz[k] * whj * (1.f - th * th);
-        dvwv_acc[k] += dcv;
-        sdcv += dcv;
-        sdw = __builtin_fmaf(s_dz[k], th, sdw);
+    for (int i = 0; i < 10; ++i) {
+      const int e = t + 256 * i;
+      if (e < P * P) {
+        const int k = e / P, j = e - k * P;
+        const float th = tanhf(VWv[((int64_t)b * P + k) * PP + j] + pgr[j]);
+        const float dcv = s_dz[k] * wh[j] * (1.f - th * th);
+        dvwv_acc[i] += dcv;
+        s_cv[e] = dcv;
+        s_tz[e] = s_dz[k] * th;
       }
-      const float ths = tanhf(PS[(int64_t)r * PP + j] + pgj);
+    }
+    __syncthreads();
+    if (t < P) {  // column j: dPG[j] = sum_k dcv[k][j] + dcs[j]; dwh[j] += sum_k dz_k tanh + dz_s tanh_s
+      const int j = t;
+      float sdcv = 0.f, sdw = 0.f;
+      for (int k = 0; k < P; ++k) {
+        sdcv += s_cv[k * P + j];
+        sdw += s_tz[k * P + j];
+      }
+      const float ths = tanhf(PS[(int64_t)r * PP + j] + pgr[j]);
       const float dcs = s_dzs * whj * (1.f - ths * ths);
       dPS[(int64_t)r * PP + j] = dcs;
       dPG[(int64_t)r * PP + j] = sdcv + dcs;
@@ -396,11 +498,20 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
 #pragma unroll
     for (int k = 0; k < P; ++k) dV[((int64_t)b * P + k) * H + d] = dv_acc[i][k];
   }
-  if (t < P) {
 #pragma unroll
-    for (int k = 0; k < P; ++k) dVWv[((int64_t)b * P + k) * PP + t] = dvwv_acc[k];
-    dwh_part[(int64_t)b * PP + t] = dwh_acc;
+  for (int i = 0; i < 10; ++i) {
+    const int e = t + 256 * i;
+    if (e < P * P) dVWv[((int64_t)b * P + e / P) * PP + e % P] = dvwv_acc[i];
   }
+  if (t < P) dwh_part[(int64_t)b * PP + t] = dwh_acc;
+}
+
+// copy a [rows][cols] matrix into pitch `pitch` (zero padding)
+__global__ void k_pad_rows(const float* __restrict__ src, int rows, int cols, int pitch, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * pitch) return;
+  const int r = (int)(i / pitch), c = (int)(i % pitch);
+  dst[i] = c < cols ? src[(int64_t)r * cols + c] : 0.f;
 }
 
 // gather rows: dst[i] = src[rows[i]]
@@ -445,22 +556,59 @@ __global__ void k_tr_cell_bwd(const float* __restrict__ dH, const float* __restr
   dc_rec[i] = dc * f_;
 }
 
-// embedding gradient: dE[v] = sum over (t, b) with tok == v of dX[t B + b][0:E], in (t, b) order
-__global__ void k_tr_embed_bwd(const int64_t* __restrict__ tok, int tld, const int* __restrict__ len, int B, int T,
-                               const float* __restrict__ dX, int E, int V, float* __restrict__ dE) {
-  const int v = blockIdx.x;
-  if (v >= V) return;
+// embedding gradient dE[v] = sum over rows r (t-major) with tok(r) == v of dX[r][0:E], in r order:
+// k_tok_rank: rank of r among the earlier rows with its token (and the token's count via the
+// first occurrence); k_tok_place: position in a token-sorted list; k_tr_embed_bwd: one
+// workgroup per row of that list that starts a token's run sums the run in order.
+__device__ __forceinline__ int tok_of(const int64_t* tok, int tld, int B, int V, int r) {
+  const int t = r / B, b = r % B;
+  int64_t tk = tok[(int64_t)b * tld + t];
+  return (int)(tk < 0 ? 0 : (tk >= V ? V - 1 : tk));
+}
+constexpr int TOK_CH = 4096;  // tokens staged per LDS pass
+__global__ void k_tok_rank(const int64_t* __restrict__ tok, int tld, int B, int R, int V, int* __restrict__ rank,
+                           int* __restrict__ count, int* __restrict__ before_tok) {
+  __shared__ int st[TOK_CH];
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int v = r < R ? tok_of(tok, tld, B, V, r) : -1;
+  int before = 0, total = 0, smaller = 0;
+  for (int c0 = 0; c0 < R; c0 += TOK_CH) {
+    const int n = R - c0 < TOK_CH ? R - c0 : TOK_CH;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) st[i] = tok_of(tok, tld, B, V, c0 + i);
+    __syncthreads();
+    for (int i = 0; i < n; ++i) {
+      const int u = st[i];
+      total += u == v;
+      before += (u == v) && (c0 + i < r);
+      smaller += u < v;
+    }
+  }
+  if (r < R) {
+    rank[r] = before;
+    count[r] = total;
+    before_tok[r] = smaller;
+  }
+}
+// order[p]: rows sorted by (token, r)
+__global__ void k_tok_place(int R, const int* __restrict__ rank, const int* __restrict__ before_tok,
+                            int* __restrict__ order) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) order[before_tok[r] + rank[r]] = r;
+}
+__global__ void k_tr_embed_bwd(const int64_t* __restrict__ tok, int tld, int B, int R, int V,
+                               const int* __restrict__ order, const int* __restrict__ rank,
+                               const int* __restrict__ count, const float* __restrict__ dX, int E,
+                               float* __restrict__ dE) {
+  const int p = blockIdx.x;  // a position in the sorted list
+  const int r0 = order[p];
+  if (rank[r0] != 0) return;  // not the first row of its token's run
+  const int v = tok_of(tok, tld, B, V, r0), n = count[r0];
   for (int e = threadIdx.x; e < E; e += blockDim.x) {
     float s = 0.f;
-    for (int t = 0; t < T; ++t)
-      for (int b = 0; b < B; ++b) {
-        int64_t tk = tok[(int64_t)b * tld + t];
-        tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
-        if (tk == v) s += dX[((int64_t)t * B + b) * 2 * E + e];
-      }
+    for (int i = 0; i < n; ++i) s += dX[(int64_t)order[p + i] * 2 * E + e];
     dE[(int64_t)v * E + e] = s;
   }
-  (void)len;
 }
 
 // dv_g[b] = sum_t dX[t B + b][E:2E] (in t order), then relu'(v_g)
@@ -496,11 +644,14 @@ __global__ void k_rowsum_pp(const float* __restrict__ X, int rows, float* __rest
 // ---------------------------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------------------------
+constexpr size_t TR_SPLIT_FLOATS = (size_t)4 << 20;  // 16 MB split-K scratch
+
 struct TrainWS {
   float *a_g, *V, *vg, *h0, *c0, *VWv, *X, *PRE, *G4, *GA, *Hs, *Cs, *SG, *S, *PG, *PS, *alpha, *beta, *ctx, *U;
   int* prow;
   // backward scratch
-  float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg;
+  float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
+  int *trank, *tcount, *torder, *tsmall;
 };
 
 static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax, size_t* bytes) {
@@ -544,6 +695,13 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.dh_rec = c.take<float>(B * H);
   w.dc_rec = c.take<float>(B * H);
   w.dvg = c.take<float>(B * E);
+  w.csum = c.take<float>((size_t)CS_CH * (d.vocab > 4 * H ? d.vocab : 4 * H));
+  w.trank = c.take<int>(R);
+  w.gsplit = c.take<float>(TR_SPLIT_FLOATS);
+  w.dsp = c.take<float>(R * (size_t)((d.vocab + 63) / 64 * 64));
+  w.tcount = c.take<int>(R);
+  w.torder = c.take<int>(R);
+  w.tsmall = c.take<int>(R);
   *bytes = c.off;
   return w;
 }
@@ -579,6 +737,7 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B;
   hipStream_t st = (hipStream_t)stream;
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS};
   // encoder tail (baseline_attention.py:46-60), reference weight layouts
   hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
   {
@@ -586,19 +745,19 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, st, feats, B, C, H, w->enc_affine_a_w,
                        w->enc_affine_a_b, s.V);
   }
-  tgemm(st, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
-  tgemm(st, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
-  tgemm(st, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
-  tgemm(st, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
+  tgemm(gc, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
+  tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
+  tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
+  tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   // x_t and the step-invariant input terms for all steps
   hipLaunchKernelGGL(k_tr_x, dim3(R), dim3(256), 0, st, tokens, tok_ld, w->embed_w, V, E, s.vg, B, T, s.X);
-  tgemm(st, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
-  tgemm(st, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
+  tgemm(gc, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
+  tgemm(gc, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
   // LSTM over T steps (baseline_attention.py:167-178)
   for (int t = 0; t < T; ++t) {
     const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
     const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
-    tgemm(st, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
+    tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
     hipLaunchKernelGGL(k_tr_cell, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.G4, s.PRE + (size_t)t * B * 5 * H,
                        5 * H, cp, B, H, s.Hs + (size_t)t * B * H, s.Cs + (size_t)t * B * H,
                        s.GA + (size_t)t * B * 4 * H);
@@ -606,16 +765,16 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
   hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
                      (int64_t)H, R, H);
-  tgemm(st, R - B, H, H, s.Hs, H, 0, w->sent_affine_h_w, H, 0, s.SG + (size_t)B * H, H, 1);
+  tgemm(gc, R - B, H, H, s.Hs, H, 0, w->sent_affine_h_w, H, 0, s.SG + (size_t)B * H, H, 1);
   hipLaunchKernelGGL(k_tr_sent, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.SG, s.Cs, s.S, (int64_t)R * H);
   // attention projections and the attention itself (adaptive_attention.py:26-58)
-  tgemm(st, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
-  tgemm(st, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
+  tgemm(gc, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
+  tgemm(gc, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
   hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs, s.S,
                      s.alpha, s.beta, s.ctx, s.U);
   // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
   hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
-  tgemm(st, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
+  tgemm(gc, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
   return aa_launch_status();
 }
 
@@ -633,14 +792,17 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B, E2 = 2 * E;
   hipStream_t st = (hipStream_t)stream;
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS};
 #define GRAD(f) (grads->f)
   const size_t RH = (size_t)R * H;
   // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)
+  const int Vp = (V + 63) / 64 * 64;  // dscores re-pitched to whole 16-B rows for vector loads
+  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp, s.dsp);
   AA_TRY(hipMemsetAsync(s.dU, 0, sizeof(float) * RH, st));
-  tgemm(st, N, H, V, dscores, V, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
+  tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
   hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
-  tgemm(st, V, H, N, dscores, V, 1, s.Up, H, 1, GRAD(mlp_w), H);
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(V)), dim3(256), 0, st, dscores, N, V, (int64_t)V, GRAD(mlp_b), 0);
+  tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
+  colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
   // Atten backward (adaptive_attention.py:26-58)
   AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
   AA_TRY(hipMemsetAsync(s.dPG, 0, sizeof(float) * (size_t)R * PP, st));
@@ -656,20 +818,20 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   }
 #undef AA_ATB
   AA_TRY(hipMemcpyAsync(s.dH, s.dU, sizeof(float) * RH, hipMemcpyDeviceToDevice, st));  // u = c_hat + h
-  tgemm(st, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
-  tgemm(st, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
-  tgemm(st, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
-  tgemm(st, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
-  tgemm(st, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
-  tgemm(st, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
+  tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
+  tgemm(gc, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
+  tgemm(gc, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
+  tgemm(gc, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
+  tgemm(gc, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
+  tgemm(gc, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
   hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(64), 0, st, s.dwh, B, GRAD(att_affine_h_w));
   // Sentinel backward (:79-83): h_{t-1} input = Hs[r - B] for r >= B, 0 for t = 0
   hipLaunchKernelGGL(k_tr_sent_bwd, dim3(nblk((int64_t)RH)), dim3(256), 0, st, s.dS, s.SG, s.Cs, s.dG, s.dC,
                      (int64_t)RH);
-  tgemm(st, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
-  tgemm(st, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
-  tgemm(st, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
-  tgemm(st, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
+  tgemm(gc, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
+  tgemm(gc, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
+  tgemm(gc, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
+  tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
   // LSTM backward through time (baseline_attention.py:167-178)
   AA_TRY(hipMemsetAsync(s.dh_rec, 0, sizeof(float) * (size_t)B * H, st));
   AA_TRY(hipMemsetAsync(s.dc_rec, 0, sizeof(float) * (size_t)B * H, st));
@@ -678,30 +840,34 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
     hipLaunchKernelGGL(k_tr_cell_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o, s.dh_rec,
                        s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H, s.DG + (size_t)t * B * 4 * H);
-    tgemm(st, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);  // dh_{t-1}
+    tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);  // dh_{t-1}
   }
-  tgemm(st, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
-  tgemm(st, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);
-  tgemm(st, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(4 * H)), dim3(256), 0, st, s.DG, R, 4 * H, (int64_t)4 * H, GRAD(lstm_b_ih), 0);
+  tgemm(gc, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
+  tgemm(gc, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);
+  tgemm(gc, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
+  colsum(st, s.DG, R, 4 * H, (int64_t)4 * H, s.csum, GRAD(lstm_b_ih));
   AA_TRY(hipMemcpyAsync(GRAD(lstm_b_hh), GRAD(lstm_b_ih), sizeof(float) * 4 * H, hipMemcpyDeviceToDevice, st));
-  tgemm(st, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
+  tgemm(gc, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
   // x_t = [embed(tok); v_g] (baseline_attention.py:151-154)
-  hipLaunchKernelGGL(k_tr_embed_bwd, dim3(V), dim3(256), 0, st, tokens, tok_ld, lengths, B, T, s.dX, E, V,
-                     GRAD(embed_w));
+  AA_TRY(hipMemsetAsync(GRAD(embed_w), 0, sizeof(float) * (size_t)V * E, st));
+  hipLaunchKernelGGL(k_tok_rank, dim3(nblk(R)), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.trank, s.tcount,
+                     s.tsmall);
+  hipLaunchKernelGGL(k_tok_place, dim3(nblk(R)), dim3(256), 0, st, R, s.trank, s.tsmall, s.torder);
+  hipLaunchKernelGGL(k_tr_embed_bwd, dim3(R), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.torder, s.trank, s.tcount,
+                     s.dX, E, GRAD(embed_w));
   hipLaunchKernelGGL(k_tr_vg_bwd, dim3(nblk((int64_t)B * E)), dim3(256), 0, st, s.dX, s.vg, B, T, E, s.dvg);
   // encoder tail (baseline_attention.py:46-60)
-  tgemm(st, E, C, B, s.dvg, E, 1, s.a_g, C, 1, GRAD(enc_affine_b_w), C);
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(E)), dim3(256), 0, st, s.dvg, B, E, (int64_t)E, GRAD(enc_affine_b_b), 0);
+  tgemm(gc, E, C, B, s.dvg, E, 1, s.a_g, C, 1, GRAD(enc_affine_b_w), C);
+  colsum(st, s.dvg, B, E, (int64_t)E, s.csum, GRAD(enc_affine_b_b));
   hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)B * H);
   hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dc_rec, s.c0, (int64_t)B * H);
-  tgemm(st, H, C, B, s.dh_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_h0_w), C);
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dh_rec, B, H, (int64_t)H, GRAD(enc_affine_h0_b), 0);
-  tgemm(st, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dc_rec, B, H, (int64_t)H, GRAD(enc_affine_c0_b), 0);
+  tgemm(gc, H, C, B, s.dh_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_h0_w), C);
+  colsum(st, s.dh_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_h0_b));
+  tgemm(gc, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);
+  colsum(st, s.dc_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_c0_b));
   hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, st, s.dV, s.V, (int64_t)B * P * H);
-  tgemm(st, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);                // dW_a = dV^T A
-  hipLaunchKernelGGL(k_colsum, dim3(nblk(H)), dim3(256), 0, st, s.dV, B * P, H, (int64_t)H, GRAD(enc_affine_a_b), 0);
+  tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);                // dW_a = dV^T A
+  colsum(st, s.dV, B * P, H, (int64_t)H, s.csum, GRAD(enc_affine_a_b));
 #undef GRAD
   return aa_launch_status();
 }

@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Training-step benchmark (BASELINE.json config 5): one train.py closure step
+of Encoder2Decoder at B=128, captions of T=18 steps (+ <start>), on 1 MI355X:
+
+    zero_grad -> forward (HIP, teacher-forced) -> CrossEntropyLoss on the packed scores
+    -> backward (HIP) -> clip_grad_norm_(LSTM, 5) -> Adam step          (train.py:197-219)
+
+Synthetic data: post-trunk features [B,2048,7,7] U[0,1), random captions with lengths 18 .. 9
+sorted descending, random-init weights of the reference architecture.  fp32 compute.  Prints ONE
+JSON line (steps/s; ms/step; the CPU oracle's autograd step timed on this host beside it).
+
+    python bench_train.py [--steps 20] [--warmup 3] [--batch 128] [--T 18] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.nn.utils.rnn import pack_padded_sequence
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
+from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
+
+
+def make_batch(B, T, seed=0):
+    rng = np.random.default_rng(seed)
+    lengths = sorted(rng.integers(T // 2, T + 1, size=B).tolist(), reverse=True)
+    lengths[0] = T
+    caps = rng.integers(2, 10123, size=(B, T + 1)).astype(np.int64)
+    caps[:, 0] = 1
+    return caps, lengths
+
+
+def step(model, opt, feats, caps, lengths):
+    model.zero_grad()
+    opt.zero_grad()
+    packed = model(feats, caps, lengths)
+    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]
+    loss = F.cross_entropy(packed[0], targets)
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+    opt.step()
+    return loss
+
+
+def cpu_baseline(caps, lengths, B, budget_s):
+    from oracle.adaptive_oracle import TrainOracle  # test / baseline infrastructure only
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    m = TrainOracle(synth.make_weights(123))
+    feats = torch.from_numpy(synth.make_features(B, seed=0))
+    capst = torch.from_numpy(caps)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 5):
+        t0 = time.perf_counter()
+        for v in m.w.values():
+            v.grad = None
+        loss, _ = m.loss(feats, capst, lengths)
+        loss.backward()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": 1.0 / med, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/adaptive_oracle.py TrainOracle forward + CE + autograd backward (PyTorch-CPU fp32, "
+                      f"reference op order) on the same B={B} batch, no optimizer; median of {len(times)} runs "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s); {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--T", type=int, default=18)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, T = args.batch, args.T
+    caps_np, lengths = make_batch(B, T)
+    model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    feats = synthetic_features(B, dev, seed=0)
+    caps = torch.from_numpy(caps_np).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    for _ in range(args.warmup):
+        step(model, opt, feats, caps, lengths)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(model, opt, feats, caps, lengths)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "training steps/s (teacher-forced fwd+bwd+Adam, B=128, T=18)", "value": args.steps / el,
+           "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": "fp32",
+           "data": "synthetic: U[0,1) post-trunk features, random captions (lengths T..T/2, sorted), random-init weights",
+           "config": {"workload": f"Encoder2Decoder.forward + CE + backward + clip + Adam, B={B}, T={T}",
+                      "batch": B, "T": T, "packed_rows": int(sum(lengths))},
+           "final_loss": float(loss.item()), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(caps_np, lengths, B, args.cpu_budget)
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
