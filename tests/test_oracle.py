@@ -55,3 +55,23 @@ def test_reference_defect_d1_shape_semantics():
     m = OracleModel(synth.make_weights(123))
     V, v_g, (h, c), a_g = m.encoder(torch.from_numpy(synth.make_features(3)))
     assert h.shape == (1, 3, 512) and c.shape == (1, 3, 512) and V.shape == (3, 49, 512) and a_g.shape == (3, 2048)
+
+
+def test_train_oracle_matches_reference_golden():
+    """TrainOracle (teacher-forced forward + CE + autograd) against the real reference's packed
+    scores, loss and gradients (tests/golden/train_b4.npz, make_golden_train.py)."""
+    from oracle.adaptive_oracle import TrainOracle
+    g = load_golden("train_b4")
+    m = TrainOracle(synth.make_weights(123, bias_noise=0.02))
+    feats = torch.from_numpy(synth.make_features(4, seed=7))
+    caps = torch.from_numpy(g["captions"])
+    loss, packed = m.loss(feats, caps, g["lengths"].tolist())
+    assert packed[1].tolist() == g["batch_sizes"].tolist()
+    np.testing.assert_allclose(packed[0].detach().numpy(), g["scores"], atol=1e-5, rtol=0)
+    assert abs(loss.item() - float(g["loss"])) <= 1e-6 * abs(float(g["loss"]))
+    loss.backward()
+    for k, p in m.w.items():
+        got = p.grad.detach().numpy().reshape(-1).astype(np.float64)
+        idx = g["g:" + k + ":idx"] if "g:" + k + ":idx" in g else slice(None)
+        ref = np.asarray(g["g:" + k], np.float64)
+        assert np.abs(got[idx] - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-30), k
