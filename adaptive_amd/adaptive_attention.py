@@ -319,6 +319,35 @@ class Encoder2Decoder(nn.Module):
         _lib.check(rc, "greedy_decode")
         return ids, alpha, beta
 
+    @torch.no_grad()
+    def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2):
+        """Beam-search decode (BASELINE config 4; not in the reference, semantics in
+        include/adaptive_amd.h and DESIGN.md) -> (ids [B,T], alpha [B,T,49], beta [B,T,1],
+        seqs [B,K,T], scores [B,K]): ids / alpha / beta of the best final beam, then every final
+        beam best first with its cumulative log-probability.  ``end_id`` = the vocabulary's
+        ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables."""
+        images = self._check_images(images)
+        model = self._model_struct()
+        lib = _lib.load()
+        B, T, K, dev = images.size(0), int(max_len), int(beam_size), images.device
+        if not 1 <= K <= _lib.MAX_BEAM:
+            raise ValueError(f"beam_size must be in [1, {_lib.MAX_BEAM}], got {K}")
+        ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+        alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+        beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+        seqs = torch.empty(B, K, T, dtype=torch.int64, device=dev)
+        scores = torch.empty(B, K, dtype=torch.float32, device=dev)
+        nbytes = lib.aa_beam_workspace_bytes(self._c_dims(), B, T, K)
+        if nbytes == 0 and B > 0 and T > 0:
+            raise ValueError(f"unsupported beam configuration B={B} T={T} K={K} for {self.dims}")
+        ws = self._workspace(nbytes, dev)
+        with torch.cuda.device(dev):
+            rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
+                                    scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
+                                    ws.numel() if ws is not None else 0, _lib.stream_handle())
+        _lib.check(rc, "beam_decode")
+        return ids, alpha, beta, seqs, scores
+
     def _lanes(self, n: int, dev) -> list:
         """n side streams on ``dev`` (created once, reused)."""
         cache = self.__dict__.setdefault("_lane_streams", {})

@@ -1,0 +1,295 @@
+// aa_beam.hip — beam-search caption decode (BASELINE config 4: B = 512,
+// beam 3).  The reference has no beam search (for_wzn:3 lists it as a TODO), so its semantics are
+// defined here and restated on the CPU by oracle/adaptive_oracle.py BeamOracle:
+//
+//   rows r = b*K + k (the K hypotheses of image b are adjacent rows, sharing V / VWv of image b)
+//   t = 0: every row holds <start> with the encoder's (h0, c0); only beam 0 is live, so the K
+//          first hypotheses are the K best first tokens of one distribution
+//   step t: logits of every row (the same AdaptiveBlock step as the greedy path), candidate score
+//          cum[k] + logp[k][v] with logp = (x - max) - log(sum exp(x - max)) (torch log_softmax);
+//          a finished beam (it emitted end_id) has exactly one candidate, end_id, at score cum[k]
+//          (it is carried unchanged); the K best candidates of the image — score descending, ties
+//          to the smaller flat index k*V + v — become the new beams
+//   end:   beams come out sorted by score; ids / alpha / beta are those of beam 0, traced back
+//          through the parent pointers.  All T steps run (as in the greedy sampler).
+//
+// Kernels: the greedy path's k_lstm (gathering h / c from each row's parent) and k_atten (kdiv =
+// K rows per image), the exact fp32 vocab GEMM k_vocab writing the logits, then k_beam_select
+// (one workgroup per image: row max / log-sum-exp / top-K in registers, K x K merge) and
+// k_beam_final (backtrace).
+namespace aa {
+
+constexpr int BEAM_MAX = 8;      // AA_MAX_BEAM
+constexpr int BEAM_VPT = 64;     // logits held per thread in k_beam_select: V <= 256 * 64
+
+// dst[r][:] = src[r / K][:]  (n a multiple of 4)
+__global__ void k_expand_rows(const float* __restrict__ src, int B, int K, int n, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  const int n4 = n / 4;
+  if (i >= (int64_t)B * K * n4) return;
+  const int64_t r = i / n4, c = i % n4;
+  reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[(r / K) * n4 + c];
+}
+
+__device__ __forceinline__ float block_max256(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__device__ __forceinline__ uint64_t block_max256_u64(uint64_t v, uint64_t* red) {
+  v = wave_max_u64(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  const uint64_t a = red[0] > red[1] ? red[0] : red[1], c = red[2] > red[3] ? red[2] : red[3];
+  return a > c ? a : c;
+}
+
+// One workgroup per image.  logits [R][V] (R = B*K); cum / fin [R] updated in place; tok / par
+// [R] = the next step's input token and parent row; htok / hpar [T][R] = history (hpar local).
+__global__ __launch_bounds__(256) void k_beam_select(int K, int V, int R, int t, int end_id,
+                                                     const float* __restrict__ logits, float* __restrict__ cum,
+                                                     int* __restrict__ fin, int64_t* __restrict__ tok,
+                                                     int* __restrict__ par, int* __restrict__ htok,
+                                                     int* __restrict__ hpar) {
+  __shared__ float redf[4];
+  __shared__ uint64_t redk[4];
+  __shared__ float s_mx[BEAM_MAX], s_ls[BEAM_MAX];
+  __shared__ uint64_t s_top[BEAM_MAX][BEAM_MAX];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  for (int k = 0; k < K; ++k) {
+    const int row = b * K + k;
+    const bool live = !(t == 0 && k > 0) && !(fin[row] != 0);  // uniform over the workgroup
+    if (!live) continue;
+    const float* x = logits + (int64_t)row * V;
+    float xs[BEAM_VPT];
+#pragma unroll
+    for (int i = 0; i < BEAM_VPT; ++i) {
+      const int c = tid + 256 * i;
+      xs[i] = c < V ? x[c] : -INFINITY;
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < BEAM_VPT; ++i) m = fmaxf(m, xs[i]);
+    m = block_max256(m, redf);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < BEAM_VPT; ++i)
+      if (tid + 256 * i < V) sum += expf(xs[i] - m);
+    sum = block_sum256(sum, redf);
+    if (tid == 0) {
+      s_mx[k] = m;
+      s_ls[k] = logf(sum);
+    }
+    // top-K of the row by (logit desc, column asc): K rounds of a block arg-max below the last key
+    uint64_t prev = ~0ull;
+    for (int j = 0; j < K; ++j) {
+      uint64_t best = 0;
+#pragma unroll
+      for (int i = 0; i < BEAM_VPT; ++i) {
+        const int c = tid + 256 * i;
+        const uint64_t key = c < V ? argmax_key(xs[i], c) : 0ull;
+        if (key < prev && key > best) best = key;
+      }
+      best = block_max256_u64(best, redk);
+      if (tid == 0) s_top[k][j] = best;
+      prev = best;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float ocum[BEAM_MAX];
+    int ofin[BEAM_MAX];
+    for (int k = 0; k < K; ++k) {
+      ocum[k] = cum[b * K + k];
+      ofin[k] = fin[b * K + k];
+    }
+    float cv[BEAM_MAX * BEAM_MAX];
+    int cf[BEAM_MAX * BEAM_MAX];
+    int n = 0;
+    for (int k = 0; k < K; ++k) {
+      if (t == 0 && k > 0) continue;
+      if (ofin[k]) {
+        cv[n] = ocum[k];
+        cf[n++] = k * V + end_id;
+        continue;
+      }
+      for (int j = 0; j < K; ++j) {
+        const int col = (int)key_token(s_top[k][j]);
+        const float xv = logits[(int64_t)(b * K + k) * V + col];
+        cv[n] = ocum[k] + ((xv - s_mx[k]) - s_ls[k]);
+        cf[n++] = k * V + col;
+      }
+    }
+    for (int j = 0; j < K; ++j) {  // selection: best remaining (score desc, flat index asc)
+      int bi = -1;
+      for (int i = 0; i < n; ++i) {
+        if (cf[i] < 0) continue;
+        if (bi < 0 || cv[i] > cv[bi] || (cv[i] == cv[bi] && cf[i] < cf[bi])) bi = i;
+      }
+      const int pk = cf[bi] / V, col = cf[bi] % V, r = b * K + j;
+      cum[r] = cv[bi];
+      fin[r] = (ofin[pk] || col == end_id) ? 1 : 0;
+      tok[r] = col;
+      par[r] = b * K + pk;
+      htok[(int64_t)t * R + r] = col;
+      hpar[(int64_t)t * R + r] = pk;
+      cf[bi] = -1;
+    }
+  }
+}
+
+// One workgroup per image: trace every final beam back (seqs [B][K][T], scores [B][K]); ids, alpha
+// and beta follow beam 0.  path [B][T] scratch: the row whose step-t attention produced beam 0's
+// token t.
+__global__ __launch_bounds__(256) void k_beam_final(int K, int T, int R, const int* __restrict__ htok,
+                                                    const int* __restrict__ hpar, const float* __restrict__ cum,
+                                                    const float* __restrict__ ahist, const float* __restrict__ bhist,
+                                                    int* __restrict__ path, int64_t* __restrict__ ids,
+                                                    int64_t* __restrict__ seqs, float* __restrict__ scores,
+                                                    float* __restrict__ alpha, float* __restrict__ beta) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid < K) {
+    int j = tid;
+    if (scores) scores[(int64_t)b * K + tid] = cum[b * K + tid];
+    for (int t = T - 1; t >= 0; --t) {
+      const int r = b * K + j;
+      const int col = htok[(int64_t)t * R + r];
+      const int pk = hpar[(int64_t)t * R + r];
+      if (seqs) seqs[((int64_t)b * K + tid) * T + t] = col;
+      if (tid == 0) {
+        if (ids) ids[(int64_t)b * T + t] = col;
+        path[(int64_t)b * T + t] = b * K + pk;
+      }
+      j = pk;
+    }
+  }
+  if (!alpha && !beta) return;
+  __syncthreads();
+  for (int i = tid; i < T * P; i += 256) {
+    const int t = i / P, q = i % P;
+    const int r = path[(int64_t)b * T + t];
+    if (alpha) alpha[((int64_t)b * T + t) * P + q] = ahist[((int64_t)t * R + r) * P + q];
+    if (beta && q == 0) beta[(int64_t)b * T + t] = bhist[(int64_t)t * R + r];
+  }
+}
+
+struct BeamWS {
+  float *a_g, *V, *vwv, *vg, *xg1, *xg, *h[2], *c[2], *s, *u, *part, *logits, *cum, *ahist, *bhist;
+  bf16x8* hsp[2];
+  int64_t *tok0, *tok;
+  int *par, *fin, *htok, *hpar, *path;
+};
+static BeamWS carve_beam(char* base, const Layout& L, int B, int T, int K, size_t* bytes) {
+  Carver c{base};
+  BeamWS w;
+  const size_t R = (size_t)B * K;
+  w.a_g = c.take<float>((size_t)B * L.C);
+  w.V = c.take<float>((size_t)B * P * L.H);
+  w.vwv = c.take<float>((size_t)B * P * PP);
+  w.vg = c.take<float>((size_t)B * L.E);
+  w.xg1 = c.take<float>((size_t)B * L.N5);
+  w.xg = c.take<float>(R * L.N5);
+  for (int i = 0; i < 2; ++i) {
+    w.h[i] = c.take<float>(R * L.H);
+    w.c[i] = c.take<float>(R * L.H);
+    w.hsp[i] = c.take<bf16x8>(hsp_frags(L, (int)R));
+  }
+  w.s = c.take<float>(R * L.H);
+  w.u = c.take<float>(R * L.H);
+  w.part = c.take<float>(R * (L.H / 16) * PART);
+  w.logits = c.take<float>(R * L.V);
+  w.cum = c.take<float>(R);
+  w.ahist = c.take<float>((size_t)T * R * P);
+  w.bhist = c.take<float>((size_t)T * R);
+  w.tok0 = c.take<int64_t>(R);
+  w.tok = c.take<int64_t>(R);
+  w.par = c.take<int>(R);
+  w.fin = c.take<int>(R);
+  w.htok = c.take<int>((size_t)T * R);
+  w.hpar = c.take<int>((size_t)T * R);
+  w.path = c.take<int>((size_t)B * T);
+  *bytes = c.off;
+  return w;
+}
+
+static int beam_check(const aa_dims* d, int B, int T, int K) {
+  if (!d) return AA_ERR_NULL;
+  if (aa_check_dims(d) != AA_OK) return AA_ERR_DIMS;
+  if (d->vocab > 256 * BEAM_VPT) return AA_ERR_DIMS;
+  if (B < 0 || T < 0 || K < 1 || K > BEAM_MAX || K > d->vocab) return AA_ERR_SHAPE;
+  if ((int64_t)B * K > (int64_t)1 << 24) return AA_ERR_SHAPE;
+  return AA_OK;
+}
+
+}  // namespace aa
+
+using namespace aa;
+
+size_t aa_beam_workspace_bytes(const aa_dims* d, int32_t B, int32_t T, int32_t K) {
+  if (beam_check(d, B, T, K) != AA_OK) return 0;
+  size_t n;
+  carve_beam(nullptr, make_layout(*d), B, T, K, &n);
+  return n;
+}
+
+int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K, int32_t end_id,
+                   int64_t* ids, int64_t* seqs, float* scores, float* alpha, float* beta, void* workspace,
+                   size_t workspace_bytes, aa_stream_t stream) {
+  Layout L;
+  int rc = check_model(m, &L);
+  if (rc) return rc;
+  rc = beam_check(&m->dims, B, T, K);
+  if (rc) return rc;
+  if (end_id >= L.V) return AA_ERR_SHAPE;
+  if (B == 0 || T == 0) return AA_OK;
+  if (!feats || !workspace) return AA_ERR_NULL;
+  if (!al16(feats) || !al16(workspace)) return AA_ERR_ALIGN;
+  size_t need;
+  BeamWS w = carve_beam(static_cast<char*>(workspace), L, B, T, K, &need);
+  if (workspace_bytes < need) return AA_ERR_BUFFER;
+  hipStream_t s = (hipStream_t)stream;
+  const MP p = resolve(m, L);
+  const int H = L.H, R = B * K;
+  // encoder tail for the B images; h0 / c0 / x_g expanded to the R = B*K rows
+  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[1], w.c[1], w.vwv, w.xg1, nullptr, 0, s);
+  if (rc) return rc;
+  auto expand = [&](const float* src, int n, float* dst) {
+    hipLaunchKernelGGL(k_expand_rows, dim3((unsigned)(((int64_t)R * (n / 4) + 255) / 256)), dim3(256), 0, s, src, B, K,
+                       n, dst);
+  };
+  expand(w.h[1], H, w.h[0]);
+  expand(w.c[1], H, w.c[0]);
+  expand(w.xg1, L.N5, w.xg);
+  hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)R * (H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], R, H,
+                     w.hsp[0]);
+  hipLaunchKernelGGL(k_fill_tok, dim3((R + 255) / 256), dim3(256), 0, s, w.tok0, R, (int64_t)1);  // <start>
+  AA_TRY(hipMemsetAsync(w.cum, 0, sizeof(float) * R, s));
+  AA_TRY(hipMemsetAsync(w.fin, 0, sizeof(int) * R, s));
+  const int MT = (R + 63) / 64;
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    lstm_atten_launch(L, p, R, t ? w.tok : w.tok0, 1, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt],
+                      w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
+                      w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K);
+    hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
+                       w.logits, (uint64_t*)nullptr);
+    hipLaunchKernelGGL(k_beam_select, dim3(B), dim3(256), 0, s, K, L.V, R, t, end_id < 0 ? -1 : end_id, w.logits,
+                       w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
+  }
+  hipLaunchKernelGGL(k_beam_final, dim3(B), dim3(256), 0, s, K, T, R, w.htok, w.hpar, w.cum, w.ahist, w.bhist, w.path,
+                     ids, seqs, scores, alpha, beta);
+  return launch_status();
+}

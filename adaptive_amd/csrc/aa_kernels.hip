@@ -478,11 +478,15 @@ __device__ __forceinline__ void x3_step(floatx16& acc, const bf16x8 (&a)[3], con
 
 constexpr int LS_CP = 68;  // k_lstm LDS tile pitch (floats): conflict-free cell reads
 
-template <int H>
+// G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
+// fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
+// gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
+template <int H, bool G = false>
 __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
-                                              const float* __restrict__ c_in, const bf16x8* __restrict__ whh3,
+                                              const float* __restrict__ c_in, const int* __restrict__ par,
+                                              const bf16x8* __restrict__ whh3,
                                               const float* __restrict__ wgs, float* __restrict__ h_out,
                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
                                               float* __restrict__ s_out, float* __restrict__ part) {
@@ -511,8 +515,20 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
   // ---- GEMM: this wave's K chunks, loads two chunks ahead ----
   constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
   const int kc0 = wave * per;
-  const bf16x8* af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
-  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
+  const bf16x8* af0;
+  const bf16x8* af1;
+  int pc = mc;  // source row of c (and of h, through the fragments)
+  if constexpr (G) {
+    const int ra0 = m0 + (lane & 31), ra1 = ra0 + 32;
+    const int p0 = par[ra0 < B ? ra0 : B - 1], p1 = par[ra1 < B ? ra1 : B - 1];
+    const int hl = 32 * (lane >> 5);
+    af0 = hsp_in + (size_t)(p0 >> 5) * KC * 3 * 64 + (p0 & 31) + hl;
+    af1 = hsp_in + (size_t)(p1 >> 5) * KC * 3 * 64 + (p1 & 31) + hl;
+    pc = par[mc];
+  } else {
+    af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+    af1 = af0 + (size_t)KC * 3 * 64;
+  }
   const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
   const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
   floatx16 acc[2][2];
@@ -554,7 +570,7 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
     }
     sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
     sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
-    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)mc * H + j);
+    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
     // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
     const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
     wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
@@ -717,8 +733,10 @@ __global__ void k_split_rows(const float* __restrict__ h, int B, int H, bf16x8* 
 // Latency structure: every load that does not depend on alpha is issued up front (this thread's V
 // columns, VWv scores operands, h, s, the partial projections), so the kernel pays ~one memory
 // latency instead of one per phase.  HPT = H / 256 columns per thread.
+// kdiv: rows per image (beam search: the beams of image b are rows b*kdiv .. b*kdiv + kdiv-1 and
+// share V / VWv of image b; 1 for the greedy path)
 template <int HPT>
-__global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __restrict__ h_new,
+__global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const float* __restrict__ h_new,
                                                const float* __restrict__ s_new, const float* __restrict__ part,
                                                const float* __restrict__ Vf, const float* __restrict__ VWv,
                                                const float* __restrict__ wh, float* __restrict__ alpha_out,
@@ -747,7 +765,8 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __re
   }
   const int k = t >> 2, q = t & 3;
   const int kc = k < P ? k : P - 1;
-  const float* vw = VWv + ((int64_t)b * P + kc) * PP;
+  const int img = kdiv == 1 ? b : b / kdiv;
+  const float* vw = VWv + ((int64_t)img * P + kc) * PP;
   float vwr[13], whr[13];
 #pragma unroll
   for (int i = 0; i < 13; ++i) {
@@ -755,7 +774,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, const float* __re
     vwr[i] = vw[j];
     whr[i] = q + 4 * i < P ? wh[j] : 0.f;  // w_h = 0 for the padding term: fma(0, tanh(.), z) == z
   }
-  const float* vb = Vf + (int64_t)b * P * H;
+  const float* vb = Vf + (int64_t)img * P * H;
   float vv[HPT][P];
 #pragma unroll
   for (int i = 0; i < HPT; ++i)
@@ -1526,16 +1545,23 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 
 
 // LSTM + attention for one step (shared by the step API and the greedy loop)
+// par != nullptr: beam search (rows continue rows par[] of the previous step; kdiv rows per image)
 static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld,
                               const float* V, const float* vwv, const float* xg, const bf16x8* hsp_in,
                               const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
                               float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
-                              const aa_trace* tr, int t, hipStream_t s) {
+                              const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1) {
   const int H = L.H, MT = (B + 63) / 64;
   rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
-#define AA_LSTM(H_)                                                                                        \
-  hipLaunchKernelGGL(k_lstm<H_>, dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, xg, hsp_in, \
-                     c_in, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part)
+#define AA_LSTM(H_)                                                                                          \
+  do {                                                                                                       \
+    if (par)                                                                                                 \
+      hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, \
+                         xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);           \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,     \
+                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);  \
+  } while (0)
   switch (H) {
     case 256: AA_LSTM(256); break;
     case 512: AA_LSTM(512); break;
@@ -1546,7 +1572,7 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
   rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
   rec(tr ? tr->atten_events : nullptr, 2 * t, s);
 #define AA_ATTEN(HPT_)                                                                                     \
-  hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, h_out, s_buf, part, V, vwv, p.wh, alpha, \
+  hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
                      alpha_ld, beta, beta_ld, u, ub, unorm)
   switch (H / 256) {
     case 1: AA_ATTEN(1); break;
@@ -1849,3 +1875,5 @@ int aa_synth_uniform(float* dst, int64_t n, uint64_t key, int64_t start, double 
 
 // teacher-forced training step (same translation unit: reuses the encoder kernels)
 #include "aa_train.hip"
+// beam-search decode (reuses k_lstm / k_atten / k_vocab and the encoder)
+#include "aa_beam.hip"

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Beam-search benchmark (BASELINE.json config 4): B=512 images, beam 3,
+max_len 20 on 1 MI355X through Encoder2Decoder.beam_search (C-ABI aa_beam_decode).
+
+Synthetic post-trunk features U[0,1) and the portable random-init weights (adaptive_amd.synth),
+inputs resident in HBM.  Prints ONE JSON line: captions/s (one caption = the best beam of one image,
+all K beams decoded), ms per batch, and the CPU restatement (oracle BeamOracle) timed on a bounded
+sample on this host.
+
+    python bench_beam.py [--steps 10] [--warmup 2] [--batch 512] [--beam 3] [--T 20] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
+from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
+
+
+def cpu_baseline(K, T, sample, budget_s):
+    from oracle.adaptive_oracle import BeamOracle  # test / baseline infrastructure only
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    m = BeamOracle(synth.make_weights(123))
+    feats = torch.from_numpy(synth.make_features(sample, seed=0))
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 5):
+        t0 = time.perf_counter()
+        m.beam_search(feats, T, K)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": sample / med, "unit": "captions/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/adaptive_oracle.py BeamOracle (PyTorch-CPU fp32, the reference decoder step) on "
+                      f"{sample} images, beam {K}, max_len {T}; median of {len(times)} runs "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s); {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--beam", type=int, default=3)
+    ap.add_argument("--T", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, K, T = args.batch, args.beam, args.T
+    model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    feats = synthetic_features(B, dev, seed=0)
+    for _ in range(args.warmup):
+        model.beam_search(feats, T, K)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = model.beam_search(feats, T, K)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"metric": f"captions/sec (beam {K}, max_len={T}) at B={B}", "value": B * args.steps / el,
+           "unit": "captions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": "fp32",
+           "data": "synthetic: U[0,1) post-trunk features, random-init weights (adaptive_amd.synth seed 123)",
+           "config": {"workload": f"Encoder2Decoder.beam_search B={B} beam={K} max_len={T}", "batch": B,
+                      "beam": K, "T": T, "rows": B * K},
+           "best_score_mean": float(out[4][:, 0].mean().item()), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(K, T, args.cpu_sample, args.cpu_budget)
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 5
+#define AA_ABI_VERSION 6
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -234,6 +234,23 @@ AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const
                              const int32_t* lengths, const float* dscores, int32_t N,
                              const aa_ref_grads* grads, void* workspace, size_t workspace_bytes,
                              aa_stream_t stream);
+
+/* ---- beam-search decode (BASELINE config 4) ------------------------------
+ * Not in the reference (its for_wzn:3 lists beam search as a TODO): semantics defined here and in
+ * oracle/adaptive_oracle.py BeamOracle.  K (1..AA_MAX_BEAM) hypotheses per image over the same
+ * decoder step as aa_greedy_decode; at step 0 only beam 0 is live; a candidate's score is the
+ * parent's cumulative score + log_softmax(logits) of the token; a beam that emitted end_id is
+ * finished and carried unchanged (its only continuation is end_id at no cost; end_id < 0: none);
+ * the K best candidates per image (score desc, ties to the smaller parent*V + token) survive.
+ * All T steps run.  Outputs (each may be NULL): ids [B,T] int64, alpha [B,T,P], beta [B,T] of the
+ * best final beam; seqs [B,K,T] int64 and scores [B,K] of all K final beams, best first.
+ * Requires vocab <= 16384.  Replaces, for beam decoding, the greedy sampler's role in coco_eval
+ * (code_src/tools/utils.py:171). */
+#define AA_MAX_BEAM 8
+AA_API size_t aa_beam_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T, int32_t K);
+AA_API int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K,
+                          int32_t end_id, int64_t* ids, int64_t* seqs, float* scores, float* alpha,
+                          float* beta, void* workspace, size_t workspace_bytes, aa_stream_t stream);
 
 /* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
  * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */

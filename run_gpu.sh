@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box driver: every GPU step under its own timeout; stop at the first crash/timeout.
-# usage: bash run_gpu.sh <step>...   steps: smoke tests testsall bench benchq prof pmc
+# usage: bash run_gpu.sh <step>...   steps: smoke tests testsall bench benchq prof pmc beamtests beambench beamprof
 set -u
 mkdir -p gpurun_out
 ok_or_fail() {  # continue on 0 (pass) or 1 (test failures); stop on crashes/timeouts
@@ -20,6 +20,10 @@ for step in "$@"; do
           timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-trace --steps 10 > gpurun_out/prof.log 2>&1; ok_or_fail $? prof ;;
     pmc)  bash tools/pmc.sh traffic fetch write; ok_or_fail $? pmc
           python tools/pmc_summary.py gpurun_out/pmc_traffic --traffic gpurun_out/traffic.json > gpurun_out/pmc_traffic/summary.txt 2>&1; cat gpurun_out/pmc_traffic/summary.txt ;;
+    beamtests) timeout -k 10 600 python -m pytest tests/test_gpu_beam.py -m gpu -q > gpurun_out/pytest_beam.log 2>&1; ok_or_fail $? beamtests; tail -25 gpurun_out/pytest_beam.log ;;
+    beambench) timeout -k 10 600 python bench_beam.py > gpurun_out/bench_beam.json 2> gpurun_out/bench_beam.err; ok_or_fail $? beambench; cat gpurun_out/bench_beam.json; tail -5 gpurun_out/bench_beam.err ;;
+    beamprof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_beam -o run --output-format csv -- python bench_beam.py --no-cpu-baseline --steps 5 > gpurun_out/prof_beam.log 2>&1; ok_or_fail $? beamprof ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

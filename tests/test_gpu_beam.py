@@ -1,0 +1,113 @@
+"""Beam-search decode (BASELINE config 4) on the GPU through the C-ABI
+(aa_beam_decode) against oracle/adaptive_oracle.py BeamOracle.
+
+The reference has no beam search (for_wzn:3 is a TODO), so BeamOracle — the reference's own
+decoder step under build-defined selection rules — is the specification: parity unpinned by the
+reference.  Sequences must be identical; cumulative scores within SCORE_TOL (a sum of T fp32
+log-probabilities whose log-sum-exp is accumulated in a different order than torch's CPU
+log_softmax); alpha / beta within 2e-5 as in the greedy tests.  Every oracle case reports its
+selection margin (smallest gap between consecutive candidates among the K+1 best), which must
+exceed the score tolerance for a sequence comparison to be meaningful."""
+import numpy as np
+import pytest
+import torch
+
+from adaptive_amd import Config, Encoder2Decoder, synth
+from oracle.adaptive_oracle import BeamOracle
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL = 5e-5
+ATT_TOL = 2e-5
+MLP_B = "decoder.adaptive.mlp.bias"
+
+
+def _weights(seed=123, end_boost=0.0):
+    sd = synth.make_weights(seed)
+    if end_boost:
+        b = sd[MLP_B].copy()
+        b[2] = np.float32(b[2] + np.float32(end_boost))  # make <end> (id 2) competitive
+        sd[MLP_B] = b
+    return sd
+
+
+def _model(dev, sd):
+    m = Encoder2Decoder(Config()).to(dev)
+    m.load_state_dict({k: torch.from_numpy(v).to(dev) for k, v in sd.items()})
+    return m
+
+
+@pytest.mark.parametrize("boost,B,T,K,fseed", [(0.0, 4, 20, 3, 0), (2.6, 8, 12, 3, 0), (2.8, 5, 10, 5, 3),
+                                               (0.0, 3, 8, 8, 1)])
+def test_beam_vs_oracle(boost, B, T, K, fseed, gpu_device):
+    sd = _weights(end_boost=boost)
+    feats = synth.make_features(B, seed=fseed)
+    o_ids, o_al, o_be, o_seqs, o_sc, margin = BeamOracle(sd).beam_search(torch.from_numpy(feats), T, K,
+                                                                         return_margin=True)
+    assert margin > 4 * SCORE_TOL, f"oracle case too close to call: margin {margin}"
+    ids, al, be, seqs, sc = _model(gpu_device, sd).beam_search(torch.from_numpy(feats).to(gpu_device), T, K)
+    assert torch.equal(seqs.cpu(), o_seqs)
+    assert torch.equal(ids.cpu(), o_ids)
+    np.testing.assert_allclose(sc.cpu().numpy(), o_sc.numpy(), atol=SCORE_TOL, rtol=0)
+    np.testing.assert_allclose(al.cpu().numpy(), o_al.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(be.cpu().numpy(), o_be.numpy(), atol=ATT_TOL, rtol=0)
+    if boost:
+        assert (o_seqs == 2).any(), "case meant to exercise finished beams has none"
+
+
+def test_beam1_equals_greedy(gpu_device):
+    """K = 1 without an end token is the greedy decode: candidate order = logit order."""
+    m = _model(gpu_device, _weights())
+    feats = synth.make_features(64, seed=2)
+    f = torch.from_numpy(feats).to(gpu_device)
+    g_ids, g_al, g_be = m.sampler(f, max_len=20)
+    ids, al, be, seqs, sc = m.beam_search(f, 20, 1, end_id=-1)
+    assert torch.equal(ids, g_ids)
+    assert torch.equal(seqs[:, 0], g_ids)
+    torch.testing.assert_close(al, g_al, atol=0, rtol=0)
+    torch.testing.assert_close(be, g_be, atol=0, rtol=0)
+
+
+def test_beam_batch_invariance(gpu_device):
+    """An image's beams do not depend on the rest of the batch (bit-exact)."""
+    m = _model(gpu_device, _weights(end_boost=2.6))
+    feats = torch.from_numpy(synth.make_features(37, seed=4)).to(gpu_device)
+    big = m.beam_search(feats, 12, 3)
+    small = m.beam_search(feats[5:9].contiguous(), 12, 3)
+    for a, b in zip(big, small):
+        assert torch.equal(a[5:9], b)
+
+
+def test_beam_b512_properties(gpu_device):
+    """Config 4 shape (B = 512, K = 3, T = 20): beams sorted, ids = best beam, finished beams stay
+    finished, the first images agree with the oracle."""
+    K, T = 3, 20
+    sd = _weights(end_boost=2.6)
+    m = _model(gpu_device, sd)
+    feats = synth.make_features(512, seed=0)
+    ids, al, be, seqs, sc = m.beam_search(torch.from_numpy(feats).to(gpu_device), T, K)
+    sc_c, seqs_c = sc.cpu(), seqs.cpu()
+    assert torch.all(sc_c[:, :-1] >= sc_c[:, 1:])
+    assert torch.equal(ids.cpu(), seqs_c[:, 0])
+    assert torch.all(sc_c <= 0)
+    ended = (seqs_c == 2).int().cummax(dim=2).values.bool()
+    assert torch.all(seqs_c[ended] == 2)
+    assert torch.allclose(al.sum(-1).cpu(), torch.ones(512, T), atol=1e-5)
+    o = BeamOracle(sd).beam_search(torch.from_numpy(feats[:6]), T, K, return_margin=True)
+    if o[5] > 4 * SCORE_TOL:
+        assert torch.equal(seqs_c[:6], o[3])
+        np.testing.assert_allclose(sc_c[:6].numpy(), o[4].numpy(), atol=SCORE_TOL, rtol=0)
+
+
+def test_beam_errors_are_loud(gpu_device):
+    m = _model(gpu_device, _weights())
+    f = torch.from_numpy(synth.make_features(2)).to(gpu_device)
+    for K in (0, 9):
+        with pytest.raises(ValueError):
+            m.beam_search(f, 5, K)
+    with pytest.raises(RuntimeError):
+        m.beam_search(f, 5, 3, end_id=10**6)
+    with pytest.raises(RuntimeError, match="GPU|CUDA"):
+        m.beam_search(f.cpu(), 5, 3)
+    out = m.beam_search(f[:0], 5, 3)
+    assert out[0].shape == (0, 5) and out[3].shape == (0, 3, 5)
