@@ -98,7 +98,7 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_size_t, c_void_p]),
     "aa_beam_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32, c_int32]),
     "aa_beam_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
-                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p]),
     "aa_vocab_logits": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_void_p]),
     "aa_vocab_logits_at": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),

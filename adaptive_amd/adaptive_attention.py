@@ -320,12 +320,15 @@ class Encoder2Decoder(nn.Module):
         return ids, alpha, beta
 
     @torch.no_grad()
-    def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2):
+    def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2,
+                    exact_vocab: bool = False):
         """Beam-search decode (BASELINE config 4; not in the reference, semantics in
         include/adaptive_amd.h and DESIGN.md) -> (ids [B,T], alpha [B,T,49], beta [B,T,1],
         seqs [B,K,T], scores [B,K]): ids / alpha / beta of the best final beam, then every final
         beam best first with its cumulative log-probability.  ``end_id`` = the vocabulary's
-        ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables."""
+        ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables.
+        ``exact_vocab``: logits from the fp32 MFMA GEMM instead of the default bf16x3 GEMM with
+        fused log-sum-exp summaries (both fp32-accurate)."""
         images = self._check_images(images)
         model = self._model_struct()
         lib = _lib.load()
@@ -344,7 +347,8 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
-                                    ws.numel() if ws is not None else 0, _lib.stream_handle())
+                                    ws.numel() if ws is not None else 0,
+                                    _lib.DECODE_EXACT_VOCAB if exact_vocab else 0, _lib.stream_handle())
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores
 

@@ -186,9 +186,276 @@ __global__ __launch_bounds__(256) void k_beam_final(int K, int T, int R, const i
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Default vocab stage: bf16x3 MFMA logits (fp32-accurate, as the encoder / LSTM GEMMs) over a 64x64
+// tile per workgroup; each wave runs the whole tile over a quarter of K (2-stage register ring of
+// fragment loads), the four partial tiles meet in LDS in a fixed order; epilogue per 32x32 block:
+// logits (+ bias) -> HBM, and per (row, 32-column granule) the pair (max, sum exp(x - max)) by a
+// transposing butterfly over the granule's 32 lanes with the online-softmax merge.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float M = fmaxf(m, m2);
+  const float a = m == -INFINITY ? 0.f : s * expf(m - M);
+  const float b = m2 == -INFINITY ? 0.f : s2 * expf(m2 - M);
+  m = M;
+  s = a + b;
+}
+template <int M>
+__device__ __forceinline__ void lse_bfly(float (&m)[16], float (&s)[16], int li) {
+  const bool hi = (li & M) != 0;
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    const float sm = hi ? m[k] : m[k + M / 2], ss = hi ? s[k] : s[k + M / 2];
+    float km = hi ? m[k + M / 2] : m[k], ks = hi ? s[k + M / 2] : s[k];
+    const float rm = __uint_as_float(partner<M>(__float_as_uint(sm)));
+    const float rs = __uint_as_float(partner<M>(__float_as_uint(ss)));
+    lse_merge(km, ks, rm, rs);
+    m[k] = km;
+    s[k] = ks;
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_vbeam3(int R, int V, int Vp, const bf16x8* __restrict__ ua3,
+                                                   const bf16x8* __restrict__ w3, const float* __restrict__ bias,
+                                                   float* __restrict__ logits, float2* __restrict__ gsum) {
+  constexpr int KC = H / 16, KW = KC / 4;  // k16 chunks per wave (even)
+  __shared__ __attribute__((aligned(16))) float Pt[2 * SC_PT];
+  const int NG = Vp / 32, NTs = Vp / 64, MT = (R + 63) / 64;
+  const int L = xcd_remap(blockIdx.x, MT * NTs);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int m0 = mt * 64, n0 = nt * 64;
+  const int kc0 = wave * KW, last = kc0 + KW - 1;
+  const bf16x8* af0 = ua3 + (size_t)(m0 >> 5) * KC * 3 * 64 + lane;
+  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
+  const bf16x8* wf0 = w3 + (size_t)(n0 >> 5) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][0][q] = af0[o];
+      fa[slot][1][q] = af1[o];
+      fw[slot][0][q] = wf0[o];
+      fw[slot][1][q] = wf1[o];
+    }
+  };
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  const int wm = wave >> 1, wn_ = wave & 1;
+  const int col = n0 + wn_ * 32 + li;
+  const float bv = bias[col];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < KW; i += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
+      const int nk = kc0 + i + d + 2;
+      load(d, nk < last ? nk : last);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // partial tiles meet in LDS ([col][row], pitch 68): ((p0 + p2) + (p1 + p3))
+  auto put = [&](float* dst) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(dst + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[a][x][4 * r4], acc[a][x][4 * r4 + 1], acc[a][x][4 * r4 + 2], acc[a][x][4 * r4 + 3]);
+  };
+  auto add = [&](const float* src) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh);
+          acc[a][x][4 * r4] += v.x; acc[a][x][4 * r4 + 1] += v.y;
+          acc[a][x][4 * r4 + 2] += v.z; acc[a][x][4 * r4 + 3] += v.w;
+        }
+  };
+  if (wave >= 2) put(Pt + (wave - 2) * SC_PT);
+  __syncthreads();
+  if (wave < 2) add(Pt + wave * SC_PT);
+  __syncthreads();
+  if (wave == 1) put(Pt);
+  __syncthreads();
+  if (wave == 0) {
+    add(Pt);
+    put(Pt);
+  }
+  __syncthreads();
+  float m[16], sm[16];
+  const bool valid = col < V;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const float4 v = *reinterpret_cast<const float4*>(Pt + (wn_ * 32 + li) * 68 + wm * 32 + 8 * r4 + 4 * lh);
+    m[4 * r4] = v.x + bv; m[4 * r4 + 1] = v.y + bv; m[4 * r4 + 2] = v.z + bv; m[4 * r4 + 3] = v.w + bv;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm * 32 + acc_row(r, lane);
+    if (row < R) logits[(int64_t)row * Vp + col] = m[r];
+    sm[r] = valid ? 1.f : 0.f;
+    m[r] = valid ? m[r] : -INFINITY;
+  }
+  lse_bfly<16>(m, sm, li);
+  lse_bfly<8>(m, sm, li);
+  lse_bfly<4>(m, sm, li);
+  lse_bfly<2>(m, sm, li);
+  float fm = m[0], fs = sm[0];
+  lse_merge(fm, fs, __uint_as_float(partner<1>(__float_as_uint(m[0]))), __uint_as_float(partner<1>(__float_as_uint(sm[0]))));
+  const int rr = (li >> 1) & 15;
+  const int row = m0 + wm * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+  if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wn_ * 32) / 32] = make_float2(fm, fs);
+}
+
+// Selection from the granule summaries: one wave per row (K waves per image).  Row log-sum-exp
+// ls = log(sum_g s_g exp(m_g - M)) (lane-strided granules in order, then the wave tree); the row's
+// top-K tokens lie in the granules whose max reaches the K-th largest granule max (ties kept), so
+// only those granules' logits are read.  Wave 0 lane 0 then merges the image's K x K candidates.
+__global__ __launch_bounds__(512) void k_beam_select3(int K, int V, int Vp, int R, int t, int end_id,
+                                                      const float* __restrict__ logits,
+                                                      const float2* __restrict__ gsum, float* __restrict__ cum,
+                                                      int* __restrict__ fin, int64_t* __restrict__ tok,
+                                                      int* __restrict__ par, int* __restrict__ htok,
+                                                      int* __restrict__ hpar) {
+  constexpr int GPL = 8;  // granule summaries held per lane: NG <= 512 (V <= 16384)
+  __shared__ float s_mx[BEAM_MAX], s_ls[BEAM_MAX];
+  __shared__ uint64_t s_top[BEAM_MAX][BEAM_MAX];
+  __shared__ int s_cand[BEAM_MAX][64 * GPL];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+  const int NG = Vp / 32;
+  const int row = b * K + k;
+  const bool live = !(t == 0 && k > 0) && fin[row] == 0;  // uniform over the wave
+  if (live) {
+    const float2* gs = gsum + (int64_t)row * NG;
+    float gm[GPL], gv[GPL];
+#pragma unroll
+    for (int i = 0; i < GPL; ++i) {
+      const int g = lane + 64 * i;
+      const float2 x = g < NG ? gs[g] : make_float2(-INFINITY, 0.f);
+      gm[i] = x.x;
+      gv[i] = x.y;
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < GPL; ++i) M = fmaxf(M, gm[i]);
+    M = wave_max(M);
+    float S = 0.f;
+#pragma unroll
+    for (int i = 0; i < GPL; ++i)
+      if (gm[i] != -INFINITY) S += gv[i] * expf(gm[i] - M);
+    S = wave_sum(S);
+    // K-th largest granule max (by value, then lower granule first)
+    uint64_t prev = ~0ull, kth = 0;
+    for (int j = 0; j < K; ++j) {
+      uint64_t best = 0;
+#pragma unroll
+      for (int i = 0; i < GPL; ++i) {
+        const int g = lane + 64 * i;
+        const uint64_t key = (g < NG && gm[i] != -INFINITY) ? argmax_key(gm[i], g) : 0ull;
+        if (key < prev && key > best) best = key;
+      }
+      best = wave_max_u64(best);
+      prev = best;
+      kth = best;
+    }
+    const float theta = key_value((uint32_t)(kth >> 32));
+    // candidate granules (gm >= theta), compacted in granule order
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < GPL; ++i) {
+      const bool c = (lane + 64 * i) < NG && gm[i] != -INFINITY && gm[i] >= theta;
+      const uint64_t bal = __ballot(c);
+      if (c) s_cand[k][n + __popcll(bal & ((1ull << lane) - 1))] = lane + 64 * i;
+      n += __popcll(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const float* x = logits + (int64_t)row * Vp;
+    prev = ~0ull;
+    for (int j = 0; j < K; ++j) {
+      uint64_t best = 0;
+      for (int e = lane; e < n * 32; e += 64) {
+        const int c = s_cand[k][e >> 5] * 32 + (e & 31);
+        const uint64_t key = c < V ? argmax_key(x[c], c) : 0ull;
+        if (key < prev && key > best) best = key;
+      }
+      best = wave_max_u64(best);
+      if (lane == 0) s_top[k][j] = best;
+      prev = best;
+    }
+    if (lane == 0) {
+      s_mx[k] = M;
+      s_ls[k] = logf(S);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float ocum[BEAM_MAX];
+    int ofin[BEAM_MAX];
+    for (int q = 0; q < K; ++q) {
+      ocum[q] = cum[b * K + q];
+      ofin[q] = fin[b * K + q];
+    }
+    float cv[BEAM_MAX * BEAM_MAX];
+    int cf[BEAM_MAX * BEAM_MAX];
+    int n = 0;
+    for (int q = 0; q < K; ++q) {
+      if (t == 0 && q > 0) continue;
+      if (ofin[q]) {
+        cv[n] = ocum[q];
+        cf[n++] = q * V + end_id;
+        continue;
+      }
+      for (int j = 0; j < K; ++j) {
+        const uint64_t key = s_top[q][j];
+        const float xv = key_value((uint32_t)(key >> 32));
+        cv[n] = ocum[q] + ((xv - s_mx[q]) - s_ls[q]);
+        cf[n++] = q * V + (int)key_token(key);
+      }
+    }
+    for (int j = 0; j < K; ++j) {
+      int bi = -1;
+      for (int i = 0; i < n; ++i) {
+        if (cf[i] < 0) continue;
+        if (bi < 0 || cv[i] > cv[bi] || (cv[i] == cv[bi] && cf[i] < cf[bi])) bi = i;
+      }
+      const int pk = cf[bi] / V, c = cf[bi] % V, r = b * K + j;
+      cum[r] = cv[bi];
+      fin[r] = (ofin[pk] || c == end_id) ? 1 : 0;
+      tok[r] = c;
+      par[r] = b * K + pk;
+      htok[(int64_t)t * R + r] = c;
+      hpar[(int64_t)t * R + r] = pk;
+      cf[bi] = -1;
+    }
+  }
+}
+
 struct BeamWS {
   float *a_g, *V, *vwv, *vg, *xg1, *xg, *h[2], *c[2], *s, *u, *part, *logits, *cum, *ahist, *bhist;
-  bf16x8* hsp[2];
+  float2* gsum;
+  bf16x8 *hsp[2], *u3;
   int64_t *tok0, *tok;
   int *par, *fin, *htok, *hpar, *path;
 };
@@ -210,7 +477,9 @@ static BeamWS carve_beam(char* base, const Layout& L, int B, int T, int K, size_
   w.s = c.take<float>(R * L.H);
   w.u = c.take<float>(R * L.H);
   w.part = c.take<float>(R * (L.H / 16) * PART);
-  w.logits = c.take<float>(R * L.V);
+  w.u3 = c.take<bf16x8>(hsp_frags(L, (int)R));
+  w.logits = c.take<float>(R * L.Vp);
+  w.gsum = c.take<float2>(R * (L.Vp / 32));
   w.cum = c.take<float>(R);
   w.ahist = c.take<float>((size_t)T * R * P);
   w.bhist = c.take<float>((size_t)T * R);
@@ -247,7 +516,7 @@ size_t aa_beam_workspace_bytes(const aa_dims* d, int32_t B, int32_t T, int32_t K
 
 int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K, int32_t end_id,
                    int64_t* ids, int64_t* seqs, float* scores, float* alpha, float* beta, void* workspace,
-                   size_t workspace_bytes, aa_stream_t stream) {
+                   size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
@@ -263,6 +532,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
   hipStream_t s = (hipStream_t)stream;
   const MP p = resolve(m, L);
   const int H = L.H, R = B * K;
+  const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   // encoder tail for the B images; h0 / c0 / x_g expanded to the R = B*K rows
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[1], w.c[1], w.vwv, w.xg1, nullptr, 0, s);
   if (rc) return rc;
@@ -283,11 +553,26 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
     const int cur = t & 1, nxt = cur ^ 1;
     lstm_atten_launch(L, p, R, t ? w.tok : w.tok0, 1, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt],
                       w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
-                      w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K);
-    hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
-                       w.logits, (uint64_t*)nullptr);
-    hipLaunchKernelGGL(k_beam_select, dim3(B), dim3(256), 0, s, K, L.V, R, t, end_id < 0 ? -1 : end_id, w.logits,
-                       w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
+                      w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K, exact ? nullptr : w.u3);
+    if (exact) {
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
+                         w.logits, (uint64_t*)nullptr);
+      hipLaunchKernelGGL(k_beam_select, dim3(B), dim3(256), 0, s, K, L.V, R, t, end_id < 0 ? -1 : end_id, w.logits,
+                         w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
+    } else {
+#define AA_VB3(H_)                                                                                            \
+  hipLaunchKernelGGL(k_vbeam3<H_>, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, L.V, L.Vp, w.u3, p.mlp_w3, p.mlp_b, \
+                     w.logits, w.gsum)
+      switch (H) {
+        case 256: AA_VB3(256); break;
+        case 512: AA_VB3(512); break;
+        case 768: AA_VB3(768); break;
+        default: AA_VB3(1024); break;
+      }
+#undef AA_VB3
+      hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
+                         w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
+    }
   }
   hipLaunchKernelGGL(k_beam_final, dim3(B), dim3(256), 0, s, K, T, R, w.htok, w.hpar, w.cum, w.ahist, w.bhist, w.path,
                      ids, seqs, scores, alpha, beta);

@@ -61,7 +61,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs;
+  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3;
   size_t total_floats;
 };
 
@@ -97,12 +97,13 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_wn = take(L.Vp);
   L.mlp_gs = take((size_t)2 * (L.Vp / VS_TILE));  // float2 per granule: (max ||w_n||, max |b_n|)
   L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
+  L.mlp_w3 = take((size_t)3 * L.Vp * L.H / 2);    // W_m as 3 bf16 planes, fragments [Vp/32][H/16][3][64][8] (beam)
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const bf16x8 *enc_w3, *whh3;
+  const bf16x8 *enc_w3, *whh3, *mlp_w3;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const float2* mlp_gs;
@@ -115,6 +116,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.enc_a_w = b + L.enc_a_w; p.enc_a_b = b + L.enc_a_b;
   p.enc_w3 = reinterpret_cast<const bf16x8*>(b + L.enc_w3);
   p.whh3 = reinterpret_cast<const bf16x8*>(b + L.whh3);
+  p.mlp_w3 = reinterpret_cast<const bf16x8*>(b + L.mlp_w3);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -742,7 +744,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
                                                const float* __restrict__ wh, float* __restrict__ alpha_out,
                                                int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
                                                float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
-                                               float* __restrict__ unorm) {
+                                               float* __restrict__ unorm, bf16x8* __restrict__ ub3_out) {
   constexpr int H = 256 * HPT;
   __shared__ float proj[PART];
   __shared__ float zs[PP];
@@ -846,6 +848,15 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
     nsq = __builtin_fmaf(u, u, nsq);
     u_out[(int64_t)b * H + d] = u;
     if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+    if (ub3_out) {  // u as 3 bf16 planes in fragment order (beam search's bf16x3 vocab GEMM)
+      __bf16 x0, x1, x2;
+      split3(u, x0, x1, x2);
+      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+      o[0] = x0;
+      o[64 * 8] = x1;
+      o[128 * 8] = x2;
+    }
   }
   if (unorm) {
     nsq = wave_sum(nsq);
@@ -1389,6 +1400,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                      reinterpret_cast<bf16x8*>(base + L.enc_w3));
   hipLaunchKernelGGL(k_pack_w3, dim3((4 * H / 32) * (H / 16)), dim3(64), 0, s, base + L.whh, H,
                      reinterpret_cast<bf16x8*>(base + L.whh3));
+  hipLaunchKernelGGL(k_pack_w3, dim3((L.Vp / 32) * (H / 16)), dim3(64), 0, s, base + L.mlp_w, H,
+                     reinterpret_cast<bf16x8*>(base + L.mlp_w3));
   return launch_status();
 }
 
@@ -1550,7 +1563,8 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
                               const float* V, const float* vwv, const float* xg, const bf16x8* hsp_in,
                               const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
                               float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
-                              const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1) {
+                              const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1,
+                              bf16x8* ub3 = nullptr) {
   const int H = L.H, MT = (B + 63) / 64;
   rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
 #define AA_LSTM(H_)                                                                                          \
@@ -1573,7 +1587,7 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
   rec(tr ? tr->atten_events : nullptr, 2 * t, s);
 #define AA_ATTEN(HPT_)                                                                                     \
   hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
-                     alpha_ld, beta, beta_ld, u, ub, unorm)
+                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
   switch (H / 256) {
     case 1: AA_ATTEN(1); break;
     case 2: AA_ATTEN(2); break;

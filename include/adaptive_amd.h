@@ -244,13 +244,16 @@ AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const
  * the K best candidates per image (score desc, ties to the smaller parent*V + token) survive.
  * All T steps run.  Outputs (each may be NULL): ids [B,T] int64, alpha [B,T,P], beta [B,T] of the
  * best final beam; seqs [B,K,T] int64 and scores [B,K] of all K final beams, best first.
+ * Logits: bf16x3 MFMA (fp32-accurate) with per-32-column (max, sum exp) summaries fused into the
+ * GEMM epilogue; flags & AA_DECODE_EXACT_VOCAB: the fp32 MFMA GEMM of aa_vocab_logits instead.
  * Requires vocab <= 16384.  Replaces, for beam decoding, the greedy sampler's role in coco_eval
  * (code_src/tools/utils.py:171). */
 #define AA_MAX_BEAM 8
 AA_API size_t aa_beam_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T, int32_t K);
 AA_API int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K,
                           int32_t end_id, int64_t* ids, int64_t* seqs, float* scores, float* alpha,
-                          float* beta, void* workspace, size_t workspace_bytes, aa_stream_t stream);
+                          float* beta, void* workspace, size_t workspace_bytes, int32_t flags,
+                          aa_stream_t stream);
 
 /* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
  * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */
