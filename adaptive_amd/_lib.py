@@ -15,7 +15,7 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 MAX_LANES = 8
@@ -95,7 +95,8 @@ SIGNATURES = {
     "aa_train_forward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p, c_int32,
                                  c_void_p, c_void_p, c_int32, c_void_p, c_size_t, c_void_p]),
     "aa_train_backward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p, c_int32,
-                                  c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_size_t, c_void_p]),
+                                  c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_void_p, c_size_t,
+                                  c_void_p]),
     "aa_beam_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32, c_int32]),
     "aa_beam_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p]),

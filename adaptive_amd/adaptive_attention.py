@@ -79,9 +79,14 @@ def _lstm_init(lstm: nn.LSTM):
 class AttentiveCNN(nn.Module):
     """Encoder tail (baseline_attention.py:11-62) over post-trunk features."""
 
-    def __init__(self, embed_size: int, hidden_size: int, cf=None, channels: int = 2048):
+    def __init__(self, embed_size: int, hidden_size: int, cf=None, channels: int = 2048, trunk: bool = False):
         super().__init__()
-        self.resnet_conv = nn.Sequential()  # trunk out of scope; identity over [B,2048,7,7]
+        # ResNet-152 trunk (adaptive_amd/trunk.py) or, by default, identity over post-trunk features
+        if trunk:
+            from .trunk import resnet_conv
+            self.resnet_conv = resnet_conv()
+        else:
+            self.resnet_conv = nn.Sequential()
         self.avgpool = nn.AvgPool2d(7)
         self.affine_a = nn.Linear(channels, hidden_size)
         self.affine_b = nn.Linear(channels, embed_size)
@@ -190,10 +195,16 @@ class Encoder2Decoder(nn.Module):
 
     MAX_PLANS = 4
 
-    def __init__(self, cf):
+    def __init__(self, cf, trunk: bool = False):
+        """``trunk=True`` adds the ResNet-152 trunk (``encoder.resnet_conv``, keys as the
+        reference's torchvision module): ``sampler`` / ``beam_search`` / ``forward`` then take images
+        [B,3,224,224]; otherwise they take post-trunk features [B,2048,7,7]."""
         nn.Module.__init__(self)
         E, H, V = cf.adaptive_word_embed_size, cf.adaptive_lstm_hidden_size, cf.vocab_length
-        self.encoder = AttentiveCNN(E, H, cf)
+        self.encoder = AttentiveCNN(E, H, cf, trunk=trunk)
+        self.has_trunk = bool(trunk)
+        self.trunk_fold = True  # eval-mode trunk runs with BatchNorm folded into the convolutions
+        self._folded = None
         self.decoder = Decoder(E, V, H, cf)
         object.__setattr__(self.encoder, "_owner", self)
         object.__setattr__(self.decoder, "_owner", self)
@@ -213,14 +224,51 @@ class Encoder2Decoder(nn.Module):
         from .synth import make_weights
         sd = make_weights(seed, self.dims, bias_noise=bias_noise)
         dev = next(self.parameters()).device
-        self.load_state_dict({k: torch.from_numpy(v).to(dev) for k, v in sd.items()}, strict=True)
+        full = {k: torch.from_numpy(v).to(dev) for k, v in sd.items()}
+        if self.has_trunk:  # the trunk keeps its own (torchvision-style random) initialisation
+            full.update({"encoder.resnet_conv." + k: v for k, v in self.encoder.resnet_conv.state_dict().items()})
+        self.load_state_dict(full, strict=True)
         return self
 
     def load_state_dict(self, state_dict, strict: bool = True, **kw):
-        # a real checkpoint (train.py:177) also carries the ResNet trunk under encoder.resnet_conv.*;
-        # the trunk is out of scope here, so those keys are dropped.
-        sd = {k: v for k, v in state_dict.items() if not k.startswith("encoder.resnet_conv.")}
+        # a real checkpoint (train.py:177) also carries the ResNet trunk under encoder.resnet_conv.*:
+        # kept when this model has the trunk, dropped when it runs on post-trunk features.
+        if self.has_trunk:
+            sd = dict(state_dict)
+        else:
+            sd = {k: v for k, v in state_dict.items() if not k.startswith("encoder.resnet_conv.")}
+        self._folded = None
         return super().load_state_dict(sd, strict=strict, **kw)
+
+    # ---- trunk (baseline_attention.py:43) -------------------------------------------------------
+    def _trunk_key(self):
+        return tuple((t.data_ptr(), t._version) for t in self.encoder.resnet_conv.state_dict().values())
+
+    def features(self, images: torch.Tensor) -> torch.Tensor:
+        """Post-trunk features A [B,2048,7,7] for images [B,3,H,W] (``resnet_conv(images)``,
+        baseline_attention.py:43) — PyTorch-ROCm convolutions (MIOpen); in eval mode without
+        autograd (sampler, beam_search) with the BatchNorms folded into the convolutions (cached
+        until a trunk tensor changes).  Without a
+        trunk, ``images`` must already be post-trunk features and are returned as they are."""
+        if not self.has_trunk or (images.dim() == 4 and images.size(1) == self.dims.channels):
+            return images
+        if images.dim() != 4 or images.size(1) != 3:
+            raise ValueError(f"images must be [B,3,H,W] (or post-trunk [B,{self.dims.channels},7,7]), got {tuple(images.shape)}")
+        if not images.is_cuda:
+            raise RuntimeError("adaptive_amd: images must be a CUDA (ROCm) tensor")
+        trunk = self.encoder.resnet_conv
+        if self.training or not self.trunk_fold or torch.is_grad_enabled():
+            A = trunk(images)  # train-mode BN, or gradients wanted: the module itself
+        else:
+            key = self._trunk_key()
+            if self._folded is None or self._folded[0] != key:
+                from .trunk import fold_bn
+                self._folded = (key, fold_bn(trunk))
+            with torch.no_grad():
+                A = self._folded[1](images.contiguous(memory_format=torch.channels_last))
+        if tuple(A.shape[1:]) != (self.dims.channels, 7, 7):
+            raise ValueError(f"trunk output {tuple(A.shape)} is not [B,{self.dims.channels},7,7] (images must be 224x224)")
+        return A.contiguous()
 
     def _c_dims(self) -> _lib.Dims:
         d = self.dims
@@ -276,7 +324,7 @@ class Encoder2Decoder(nn.Module):
         row blocks so the lanes' kernels overlap; captions are independent, results are identical.
         ``graph`` (default ``self.decode_graph``): repeated calls on the same input buffer replay a
         captured hipGraph of the whole decode (C-ABI aa_decode_plan); results are identical."""
-        images = self._check_images(images)
+        images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
         B, T, dev = images.size(0), int(max_len), images.device
@@ -329,7 +377,7 @@ class Encoder2Decoder(nn.Module):
         ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables.
         ``exact_vocab``: logits from the fp32 MFMA GEMM instead of the default bf16x3 GEMM with
         fused log-sum-exp summaries (both fp32-accurate)."""
-        images = self._check_images(images)
+        images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
         B, T, K, dev = images.size(0), int(max_len), int(beam_size), images.device
@@ -373,7 +421,7 @@ class Encoder2Decoder(nn.Module):
     # ---- AttentiveCNN.forward (baseline_attention.py:36-62) -------------------------------------
     @torch.no_grad()
     def _encode(self, images: torch.Tensor):
-        images = self._check_images(images)
+        images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
         d, B, dev = self.dims, images.size(0), images.device
@@ -455,9 +503,11 @@ class Encoder2Decoder(nn.Module):
         ``pack_padded_sequence(scores, lengths, batch_first=True)``; differentiable w.r.t. every
         parameter (HIP forward and backward kernels, C-ABI ``aa_train_*``), so train.py's closure
         (CrossEntropyLoss on ``packed[0]``, ``loss.backward()``, clip_grad_norm_, optimizer.step)
-        runs unchanged.  ``images`` are post-trunk features [B,2048,7,7]."""
+        runs unchanged.  ``images`` are post-trunk features [B,2048,7,7], or images [B,3,224,224]
+        when the model has the trunk (its forward and backward then run in PyTorch-ROCm and the
+        HIP backward hands it dL/dA, so CNN fine-tuning, train.py:89, works unchanged)."""
         from torch.nn.utils.rnn import PackedSequence
-        images = self._check_images(images)
+        images = self._check_images(self.features(images))
         lengths = [int(n) for n in (lengths.tolist() if torch.is_tensor(lengths) else lengths)]
         B = images.size(0)
         if captions.dim() != 2 or captions.size(0) != B or len(lengths) != B:
@@ -506,15 +556,16 @@ class _TeacherForced(torch.autograd.Function):
         B = images.size(0)
         dscores = dscores.contiguous().float()
         grads = [torch.empty_like(p) for p in params]
+        dfeats = torch.empty_like(images) if ctx.needs_input_grad[1] else None
         w = _lib.RefWeights(*[p.data_ptr() for p in params])
         g = _lib.RefWeights(*[t.data_ptr() for t in grads])
         with torch.cuda.device(images.device):
             rc = lib.aa_train_backward(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(), caps.stride(0),
-                                       len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g, ctx.ws.data_ptr(),
-                                       ctx.ws.numel(), _lib.stream_handle())
+                                       len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g, _lib.ptr(dfeats),
+                                       ctx.ws.data_ptr(), ctx.ws.numel(), _lib.stream_handle())
         _lib.check(rc, "train_backward")
         ctx.ws = None
-        return (None, None, None, None, None, None, *grads)
+        return (None, dfeats, None, None, None, None, *grads)
 
 
 def synthetic_features(B: int, device, seed: int = 0, row0: int = 0, dims: Dims = Dims()) -> torch.Tensor:

@@ -622,6 +622,24 @@ __global__ void k_tr_vg_bwd(const float* __restrict__ dX, const float* __restric
   dvg[i] = vg[i] > 0.f ? s : 0.f;
 }
 
+// dL/dA for the trunk (NCHW, baseline_attention.py:43-51): dfeats[b][c][p] = dA[b*49 + p][c] +
+// dag[b][c] / 49 (AvgPool2d(7)'s gradient spreads d a_g evenly).  Tiles of 49 x 64 through LDS so
+// both the read (along c) and the write (along p) are coalesced.
+__global__ __launch_bounds__(256) void k_dfeats(const float* __restrict__ dA, const float* __restrict__ dag, int C,
+                                                float* __restrict__ dfeats) {
+  __shared__ float tile[P][65];
+  const int b = blockIdx.y, c0 = blockIdx.x * 64, t = threadIdx.x;
+  for (int i = t; i < P * 64; i += 256) {
+    const int p = i / 64, c = i % 64;
+    tile[p][c] = c0 + c < C ? dA[((int64_t)b * P + p) * C + c0 + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = t; i < 64 * P; i += 256) {
+    const int c = i / P, p = i % P;
+    if (c0 + c < C) dfeats[((int64_t)b * C + c0 + c) * P + p] = tile[p][c] + dag[(int64_t)b * C + c0 + c] / 49.f;
+  }
+}
+
 // elementwise helpers
 __global__ void k_relu_mask(float* __restrict__ d, const float* __restrict__ y, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -651,6 +669,7 @@ struct TrainWS {
   int* prow;
   // backward scratch
   float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
+  float *dA, *dag;  // d(features) pieces: through V [B*49][C] and through a_g [B][C]
   int *trank, *tcount, *torder, *tsmall;
 };
 
@@ -695,6 +714,8 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.dh_rec = c.take<float>(B * H);
   w.dc_rec = c.take<float>(B * H);
   w.dvg = c.take<float>(B * E);
+  w.dA = c.take<float>(B * P_ * Cc);
+  w.dag = c.take<float>(B * Cc);
   w.csum = c.take<float>((size_t)CS_CH * (d.vocab > 4 * H ? d.vocab : 4 * H));
   w.trank = c.take<int>(R);
   w.gsplit = c.take<float>(TR_SPLIT_FLOATS);
@@ -780,7 +801,8 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
 
 int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
                       const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, const float* dscores, int32_t N,
-                      const aa_ref_grads* grads, void* workspace, size_t workspace_bytes, aa_stream_t stream) {
+                      const aa_ref_grads* grads, float* dfeats, void* workspace, size_t workspace_bytes,
+                      aa_stream_t stream) {
   using namespace aa;
   int rc = train_check(dims, B, T);
   if (rc) return rc;
@@ -868,6 +890,13 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, st, s.dV, s.V, (int64_t)B * P * H);
   tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);                // dW_a = dV^T A
   colsum(st, s.dV, B * P, H, (int64_t)H, s.csum, GRAD(enc_affine_a_b));
+  if (dfeats) {  // gradient into the trunk's output A (CNN fine-tuning, train.py:89)
+    tgemm(gc, B * P, C, H, s.dV, H, 0, w->enc_affine_a_w, C, 1, s.dA, C);              // dA = dV W_a
+    tgemm(gc, B, C, E, s.dvg, E, 0, w->enc_affine_b_w, C, 1, s.dag, C);                // d a_g = dv_g W_b
+    tgemm(gc, B, C, H, s.dh_rec, H, 0, w->enc_affine_h0_w, C, 1, s.dag, C, 1);         //   + dh0 W_h0
+    tgemm(gc, B, C, H, s.dc_rec, H, 0, w->enc_affine_c0_w, C, 1, s.dag, C, 1);         //   + dc0 W_c0
+    hipLaunchKernelGGL(k_dfeats, dim3((C + 63) / 64, B), dim3(256), 0, st, s.dA, s.dag, C, dfeats);
+  }
 #undef GRAD
   return aa_launch_status();
 }

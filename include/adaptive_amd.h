@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 6
+#define AA_ABI_VERSION 7
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -222,7 +222,8 @@ AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
  * aa_train_forward writes the packed scores [N][V] (pack_padded_sequence(scores, lengths).data:
  * rows t-major over the batch entries still running at step t) and keeps the activations in the
  * workspace; aa_train_backward takes dL/dscores [N][V] with the same arguments and workspace and
- * writes the gradient of every parameter (assigned, not accumulated).  The reference's loss
+ * writes the gradient of every parameter (assigned, not accumulated), and, if dfeats is not NULL,
+ * dL/dfeats [B,C,7,7] (the gradient into the ResNet trunk's output, for CNN fine-tuning).  The reference's loss
  * (train.py: CrossEntropyLoss on the packed scores) stays with the caller. */
 AA_API size_t aa_train_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
 AA_API int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B,
@@ -232,8 +233,8 @@ AA_API int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const 
 AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats,
                              int32_t B, int32_t T, const int64_t* tokens, int32_t tok_ld,
                              const int32_t* lengths, const float* dscores, int32_t N,
-                             const aa_ref_grads* grads, void* workspace, size_t workspace_bytes,
-                             aa_stream_t stream);
+                             const aa_ref_grads* grads, float* dfeats, void* workspace,
+                             size_t workspace_bytes, aa_stream_t stream);
 
 /* ---- beam-search decode (BASELINE config 4) ------------------------------
  * Not in the reference (its for_wzn:3 lists beam search as a TODO): semantics defined here and in

@@ -91,6 +91,31 @@ def test_train_step_vs_oracle_ragged(gpu_device):
         _grad_close(got, oracle.w[k].grad.detach().numpy(), k)
 
 
+def test_train_feature_gradient_vs_oracle(gpu_device):
+    """dL/dA into the trunk's output (aa_train_backward's dfeats, CNN fine-tuning, train.py:89)
+    against the oracle's autograd, on the ragged B = 13 batch."""
+    from oracle.adaptive_oracle import TrainOracle
+    B, L = 13, 12
+    lengths = [9, 9, 8, 7, 7, 6, 5, 4, 4, 3, 2, 1, 1]
+    rng = np.random.default_rng(5)
+    caps_np = rng.integers(0, 10123, size=(B, L)).astype(np.int64)
+    caps_np[:, 0] = 1
+    state = synth.make_weights(31, bias_noise=0.01)
+    feats_np = synth.make_features(B, seed=9)
+    ref_feats = torch.from_numpy(feats_np).requires_grad_(True)
+    rloss, _ = TrainOracle(state).loss(ref_feats, torch.from_numpy(caps_np), lengths)
+    rloss.backward()
+    model = _model(gpu_device, seed=31, noise=0.01)
+    feats = torch.from_numpy(feats_np).to(gpu_device).requires_grad_(True)
+    loss, _ = _loss(model, feats, torch.from_numpy(caps_np).to(gpu_device), lengths)
+    loss.backward()
+    # every V entry within rounding of the ReLU kink that lands on the other side moves a whole
+    # W_a row (2048 entries) of dA, so the Frobenius bound is 3x the parameter-gradient one here
+    got, ref = feats.grad.cpu().double().numpy(), ref_feats.grad.double().numpy()
+    assert np.abs(got - ref).max() <= GRAD_ENTRY * np.abs(ref).max()
+    assert np.linalg.norm(got - ref) <= 3 * GRAD_REL * np.linalg.norm(ref)
+
+
 def test_train_step_deterministic(gpu_device):
     g = load_golden("train_b4")
     feats = torch.from_numpy(synth.make_features(4, seed=7)).to(gpu_device)
