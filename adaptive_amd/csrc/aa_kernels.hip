@@ -866,6 +866,141 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   }
 }
 
+// k_atten with two threads per output dimension's worth of parallelism: 512 threads per row, each
+// owning H/512 dimensions of the context (half the V registers of k_atten<2>, twice the waves in
+// flight per CU), the 32 projection partials summed by four groups of 128 threads (8 each, then
+// (g0 + g1) + (g2 + g3)), and each of the 50 scores by 8 lanes (7 terms each, xor-butterfly
+// combine).  Same outputs as k_atten; rounding of the projections / scores differs (fixed orders).
+template <int H>
+__global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __restrict__ h_new,
+                                                const float* __restrict__ s_new, const float* __restrict__ part,
+                                                const float* __restrict__ Vf, const float* __restrict__ VWv,
+                                                const float* __restrict__ wh, float* __restrict__ alpha_out,
+                                                int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
+                                                float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
+                                                float* __restrict__ unorm, bf16x8* __restrict__ ub3_out) {
+  constexpr int DPT = H / 512, NT16 = H / 16, NG = NT16 / 4;
+  __shared__ float red[4][128];
+  __shared__ float proj[PART];
+  __shared__ float zs[PP];
+  __shared__ float sh_alpha[PP];
+  __shared__ float sh_beta;
+  __shared__ float sh_norm[8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = blockIdx.x;
+  const int img = kdiv == 1 ? b : b / kdiv;
+  // loads, oldest first in the order they are consumed; clamped addresses, no branches
+  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
+  float pv[NG];
+  {
+    const float* pp = part + ((int64_t)b * NT16 + grp) * PART + jpc;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) pv[i] = pp[(int64_t)4 * i * PART];
+  }
+  const int k = t >> 3, q = t & 7;
+  const int kc = k < P ? k : P - 1;
+  const float* vw = VWv + ((int64_t)img * P + kc) * PP;
+  float vwr[7], whr[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+    vwr[i] = vw[j];
+    whr[i] = q + 8 * i < P ? wh[j] : 0.f;
+  }
+  const float* vb = Vf + (int64_t)img * P * H;
+  float vv[DPT][P];
+#pragma unroll
+  for (int i = 0; i < DPT; ++i)
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
+  float hv[DPT], sv[DPT];
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    hv[i] = h_new[(int64_t)b * H + t + 512 * i];
+    sv[i] = s_new[(int64_t)b * H + t + 512 * i];
+  }
+  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
+  {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) a += pv[i];
+    red[grp][jp] = a;
+  }
+  __syncthreads();
+  if (t < 2 * P) proj[t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  __syncthreads();
+  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+      const float x = (k < P ? vwr[i] : proj[P + j]) + proj[j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
+    }
+    z = z + __shfl_xor(z, 1, 64);
+    z = z + __shfl_xor(z, 2, 64);
+    z = z + __shfl_xor(z, 4, 64);
+    if (q == 0 && k <= P) zs[k] = z;
+  }
+  __syncthreads();
+  // 3) softmax (wave 0)
+  if (w == 0) {
+    const float z = lane < P ? zs[lane] : -INFINITY;
+    const float zsn = zs[P];
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float S = wave_sum(e);
+    const float a = e / S;
+    if (lane < P) {
+      sh_alpha[lane] = a;
+      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
+    }
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      const float beta = es / S2;
+      sh_beta = beta;
+      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
+    }
+  }
+  __syncthreads();
+  // 4) context + u
+  const float beta = sh_beta;
+  float nsq = 0.f;
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int d = t + 512 * i;
+    float c = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sh_alpha[kk], vv[i][kk], c);
+    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
+    const float u = chat + hv[i];
+    nsq = __builtin_fmaf(u, u, nsq);
+    u_out[(int64_t)b * H + d] = u;
+    if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+    if (ub3_out) {
+      __bf16 x0, x1, x2;
+      split3(u, x0, x1, x2);
+      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+      o[0] = x0;
+      o[64 * 8] = x1;
+      o[128 * 8] = x2;
+    }
+  }
+  if (unorm) {
+    nsq = wave_sum(nsq);
+    if (lane == 0) sh_norm[w] = nsq;
+    __syncthreads();
+    if (t == 0)
+      unorm[b] = sqrtf(((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) +
+                       ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.00001f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a
 // 128x128 tile, then per (row, 32-column granule g) with the granule's bound E (see CEPS):
@@ -1588,13 +1723,17 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
 #define AA_ATTEN(HPT_)                                                                                     \
   hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
                      alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
-  switch (H / 256) {
-    case 1: AA_ATTEN(1); break;
-    case 2: AA_ATTEN(2); break;
-    case 3: AA_ATTEN(3); break;
-    default: AA_ATTEN(4); break;
+#define AA_ATTEN5(H_)                                                                                      \
+  hipLaunchKernelGGL(k_atten5<H_>, dim3(B), dim3(512), 0, s, B, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
+                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+  switch (H) {
+    case 256: AA_ATTEN(1); break;
+    case 512: AA_ATTEN5(512); break;
+    case 768: AA_ATTEN(3); break;
+    default: AA_ATTEN5(1024); break;
   }
 #undef AA_ATTEN
+#undef AA_ATTEN5
   rec(tr ? tr->atten_events : nullptr, 2 * t + 1, s);
 }
 

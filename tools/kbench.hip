@@ -28,6 +28,9 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
     } else if (!strcmp(which, "atten")) {
       hipLaunchKernelGGL(k_atten<2>, dim3(B), dim3(256), 0, s, B, H / 16, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
                          (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
+    } else if (!strcmp(which, "atten5")) {
+      hipLaunchKernelGGL(k_atten5<512>, dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
+                         (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
     } else if (!strcmp(which, "vscreen")) {
       hipLaunchKernelGGL(k_vscreen<512>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V,
                          L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,
