@@ -1973,6 +1973,15 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
     plan_free(p);
     return rc;
   }
+  // the capture streams are not needed to replay the graph: release them (and their hardware
+  // queues -- HIP maps streams onto a few queues per process, and idle streams crowd them)
+  (void)hipStreamDestroy(p->cap);
+  (void)hipStreamDestroy(p->aux);
+  p->cap = p->aux = nullptr;
+  for (int i = 0; i < p->n_lanes; ++i) {
+    (void)hipStreamDestroy(p->lanes[i]);
+    p->lanes[i] = nullptr;
+  }
   *out = p;
   return AA_OK;
 }

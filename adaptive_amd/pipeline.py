@@ -1,0 +1,116 @@
+"""Pipelined greedy decode over a stream of batches — the reference's evaluation loop
+(``coco_eval``: ``for images in data_loader: model.sampler(images)``, code_src/tools/utils.py:167-171)
+with up to ``depth`` batches in flight on their own HIP streams.
+
+One B = 512 decode is latency-bound on MI355X: its step kernels hold one or two workgroups per CU,
+and the encoder GEMM cannot start before the previous batch's last step.  Batches are independent,
+so batch i + 1 (encoder and first steps) runs on a second stream while batch i finishes: same
+kernels, same per-batch work and the same ids bit for bit (tests/test_gpu_parity.py), more of the
+chip busy.  Each slot owns its stream, workspace (or captured decode plan) and output buffers; the
+caller's stream waits for a batch's completion event only when that batch's result is handed out.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Iterable, Iterator, Tuple
+
+import torch
+
+from . import _lib
+from .adaptive_attention import ATT, _Plan
+
+
+class _Slot:
+    def __init__(self, dev):
+        self.stream = torch.cuda.Stream(device=dev)
+        self.ws = None
+        self.plans = collections.OrderedDict()  # images key -> _Plan
+        self.seen = set()
+
+
+class DecodePipeline:
+    """``for ids, alpha, beta in DecodePipeline(model, max_len=20).run(batches): ...`` — results
+    in submission order, each exactly ``model.sampler(images, max_len)``'s.
+
+    ``graph=False`` (default) launches each batch's kernels directly into its slot's stream: the
+    process then owns exactly ``depth`` busy streams.  HIP multiplexes a process's streams onto a
+    few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and two slots that land on one queue
+    serialise; captured plans (``graph=True``) add the graph executor's own branch streams to that
+    count, which made the overlap hit-or-miss in measurements."""
+
+    MAX_PLANS = 2
+
+    def __init__(self, model, max_len: int = 20, depth: int = 2, graph: bool = False):
+        if depth < 1:
+            raise ValueError("depth must be >= 1")
+        self.model, self.T, self.depth, self.graph = model, int(max_len), int(depth), bool(graph)
+        self._slots = None
+        self._pending = collections.deque()
+        self._n = 0
+
+    def _slot(self, dev) -> _Slot:
+        if self._slots is None:
+            self._slots = [_Slot(dev) for _ in range(self.depth)]
+        return self._slots[self._n % self.depth]
+
+    @torch.no_grad()
+    def submit(self, images: torch.Tensor) -> None:
+        """Queue one batch (post-trunk features, or images when the model has the trunk)."""
+        m = self.model
+        if len(self._pending) >= self.depth:
+            raise RuntimeError("pipeline full: retire() a result first")
+        images = m._check_images(m.features(images))
+        model = m._model_struct()  # (re)packs on the current stream if the weights changed
+        lib = _lib.load()
+        B, T, dev = images.size(0), self.T, images.device
+        slot = self._slot(dev)
+        ready = torch.cuda.Event()
+        ready.record()  # images (and any repack) are ready on the caller's stream
+        s = slot.stream
+        s.wait_event(ready)
+        images.record_stream(s)
+        with torch.cuda.device(dev), torch.cuda.stream(s):
+            key = (images.data_ptr(), B, T, m._packed.data_ptr())
+            plan = slot.plans.get(key) if self.graph else None
+            if plan is None and self.graph and key in slot.seen and B > 0 and T > 0:
+                s.synchronize()
+                plan = slot.plans[key] = _Plan(lib, model, images, B, T, 0, 1, m._c_dims(), dev)
+                while len(slot.plans) > self.MAX_PLANS:
+                    slot.plans.popitem(last=False)
+            slot.seen.add(key)
+            if plan is not None:
+                _lib.check(lib.aa_decode_plan_launch(plan.handle, s.cuda_stream), "decode_plan_launch")
+                out = (plan.ids.clone(), plan.alpha.clone(), plan.beta.clone())
+            else:
+                ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+                alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+                beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+                nbytes = lib.aa_decode_workspace_bytes(m._c_dims(), B, T)
+                if nbytes and (slot.ws is None or slot.ws.numel() < nbytes):
+                    slot.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                          beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None, 0,
+                                          s.cuda_stream)
+                _lib.check(rc, "greedy_decode")
+                out = (ids, alpha, beta)
+            done = torch.cuda.Event()
+            done.record(s)
+        self._pending.append((done, out, images))
+        self._n += 1
+
+    def retire(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """The oldest queued batch's (ids, alpha, beta); the caller's stream waits for it."""
+        done, out, _ = self._pending.popleft()
+        cur = torch.cuda.current_stream()
+        cur.wait_event(done)
+        for t in out:
+            t.record_stream(cur)
+        return out
+
+    def run(self, batches: Iterable[torch.Tensor]) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        for images in batches:
+            if len(self._pending) >= self.depth:
+                yield self.retire()
+            self.submit(images)
+        while self._pending:
+            yield self.retire()

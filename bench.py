@@ -18,6 +18,7 @@ restatement of the reference sampler, oracle/adaptive_oracle.py, timed on this h
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -34,6 +35,7 @@ from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
 from adaptive_amd import _lib  # noqa: E402
 from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
 from adaptive_amd.hip_events import EventArray  # noqa: E402
+from adaptive_amd.pipeline import DecodePipeline  # noqa: E402
 
 METRIC = "captions/sec (greedy, max_len=20) at B=512; 1/2/4/8-GPU scaling"
 PEAK_FP32 = 157.3e12     # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
@@ -125,6 +127,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch kernels directly instead of replaying the "
                     "captured decode plan (hipGraph)")
     ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
+    ap.add_argument("--pipeline-depth", type=int, default=2, help="batches in flight in the headline region "
+                    "(adaptive_amd.pipeline.DecodePipeline: batch i+1 starts on its own stream while batch i "
+                    "finishes); 1 = one sampler() call after another")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -150,8 +155,17 @@ def main():
             dist.all_gather_into_tensor(ids_all, ids)
         return ids
 
+    depth = max(1, args.pipeline_depth)
+    pipe = DecodePipeline(model, max_len=T, depth=depth)
+
+    def pipelined(n):
+        for ids, _, _ in pipe.run(itertools.repeat(feats, n)):
+            if world > 1:
+                dist.all_gather_into_tensor(ids_all, ids)
+
     for _ in range(args.warmup):
         step()
+    pipelined(max(args.warmup, 2 * depth + 1))  # every slot sees the input twice: its plan is captured
     K = args.steps
     traces = []
     if not args.no_trace:
@@ -160,14 +174,17 @@ def main():
             ev["encoder"] = EventArray(2 * _lib.TRACE_ENCODER_KERNELS)
             tr = _lib.Trace(ev["encoder"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["screen"].ptr, ev["rescore"].ptr)
             traces.append((ev, tr))
-    def timed(trace_list):
+    def timed(trace_list, pipeline=False):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for k in range(K):
-            step(trace_list[k][1] if trace_list else None)
+        if pipeline:
+            pipelined(K)
+        else:
+            for k in range(K):
+                step(trace_list[k][1] if trace_list else None)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -182,7 +199,10 @@ def main():
     # HIP event pair around every kernel launch (on the launch stream) for the per-kernel averages;
     # each event is a timestamp packet in the queue, so region 2 runs a little slower and is
     # reported separately as ``traced_ms_per_step``.
-    elapsed = timed(None)
+    # Region 0: the same K batches through DecodePipeline (depth batches in flight) -- the headline
+    # when depth > 1; region 1 (sequential sampler calls) is reported beside it.
+    elapsed_seq = timed(None)
+    elapsed = timed(None, pipeline=True) if depth > 1 else elapsed_seq
     traced_elapsed = timed(traces) if traces else None
     captions = world * B * K
     value = captions / elapsed
@@ -249,7 +269,9 @@ def main():
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
                    "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else ""),
                    "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
-                   "hip_graph": not args.no_graph},
+                   "hip_graph": not args.no_graph, "batches_in_flight": depth},
+        "sequential": {"value": world * B * K / elapsed_seq, "ms_per_step": 1e3 * elapsed_seq / K,
+                       "note": "one sampler() call after another (batches_in_flight = 1)"},
         "roofline": roofline,
         "path_roofline": {"bound": "mfma", "achieved": fl["total"] * value / 1e12, "peak": PEAK_FP32 / 1e12,
                           "unit": "TFLOP/s", "frac": fl["total"] * value / PEAK_FP32,

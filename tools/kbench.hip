@@ -8,6 +8,223 @@
 
 using namespace aa;
 
+namespace aa {
+// VARIANTS BEGIN
+template <int MODE>
+__global__ __launch_bounds__(512) void kv_ls(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+                                              const float* __restrict__ table,
+                                              const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
+                                              const float* __restrict__ c_in, const int* __restrict__ par,
+                                              const bf16x8* __restrict__ whh3,
+                                              const float* __restrict__ wgs, float* __restrict__ h_out,
+                                              bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                              float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int H = 512; constexpr bool G = false;
+  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
+  constexpr int WSP = 100;  // 98 projection outputs padded to whole float4s
+  __shared__ __attribute__((aligned(16))) float lds[8 * TS + 2 * 64 * 16 + 16 * WSP];
+  constexpr int NTn = H / 16, KC = H / 16;
+  const int MT = (B + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = mt * BM;
+  float* Pt = lds;                 // [8][64][CP] partial tiles; slot 0 becomes the summed tile
+  float* Hs = Pt + 8 * TS;         // [64][16] h' of the tile
+  float* Ss = Hs + 64 * 16;        // [64][16] s of the tile
+  float* Wsl = Ss + 64 * 16;       // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
+
+  // cell-epilogue mapping: thread -> row rr, units u0, u0 + 1 of the tile
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
+  const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
+  const int j = nt * 16 + u0;
+  // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
+  //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
+  int64_t tk = tok[(int64_t)mc * tok_ld];
+
+  // ---- GEMM: this wave's K chunks, loads two chunks ahead ----
+  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
+  const int kc0 = wave * per;
+  const bf16x8* af0;
+  const bf16x8* af1;
+  int pc = mc;  // source row of c (and of h, through the fragments)
+  if constexpr (G) {
+    const int ra0 = m0 + (lane & 31), ra1 = ra0 + 32;
+    const int p0 = par[ra0 < B ? ra0 : B - 1], p1 = par[ra1 < B ? ra1 : B - 1];
+    const int hl = 32 * (lane >> 5);
+    af0 = hsp_in + (size_t)(p0 >> 5) * KC * 3 * 64 + (p0 & 31) + hl;
+    af1 = hsp_in + (size_t)(p1 >> 5) * KC * 3 * 64 + (p1 & 31) + hl;
+    pc = par[mc];
+  } else {
+    af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+    af1 = af0 + (size_t)KC * 3 * 64;
+  }
+  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][0][q] = af0[o];
+      fa[slot][1][q] = af1[o];
+      fw[slot][0][q] = wf0[o];
+      fw[slot][1][q] = wf1[o];
+    }
+  };
+  const int last = kc0 + per - 1;
+  asm volatile("" ::: "memory");
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
+  float2 ta[4], xa[4], sa, sb, cprev;
+  float4 wsv;
+  {
+    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+    const int N5 = 5 * H;
+    const float* trow = table + tk * N5;
+    const float* xrow = xg + (int64_t)mc * N5;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
+    }
+    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+    sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
+    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
+    // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
+    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+    wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < per; i += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) if (MODE != 1) x3_step(acc[a][c], fa[d][a], fw[d][c]); else acc[a][c][0] += fa[d][a][0][0] == fw[d][c][0][0] ? 1.f : 0.f;
+      const int nk = kc0 + i + d + 2;
+      load(d, nk < last ? nk : last);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // ---- partial tiles -> LDS, fixed-tree sum into slot 0 ----
+  {
+    float* dst = Pt + wave * TS;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31)] = acc[a][c][r];
+  }
+  {  // transpose the W_g / W_s slice to [unit][j] (j = 98, 99 are zero)
+    const int jj = t >> 2, uq = (t & 3) * 4;
+    if (t < 2 * P * 4) {
+      Wsl[(uq + 0) * WSP + jj] = wsv.x; Wsl[(uq + 1) * WSP + jj] = wsv.y;
+      Wsl[(uq + 2) * WSP + jj] = wsv.z; Wsl[(uq + 3) * WSP + jj] = wsv.w;
+    } else if (t < 2 * P * 4 + 32) {
+      const int z = t - 2 * P * 4;  // 32 zeros: j = 98, 99 for 16 units
+      Wsl[(z >> 1) * WSP + 2 * P + (z & 1)] = 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
+    const int q = t + 512 * i, r = q >> 4, c4 = (q & 15) * 4;
+    const float* sp = Pt + r * CP + c4;
+    float4 v[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v[w] = *reinterpret_cast<const float4*>(sp + (MODE == 3 ? 0 : w) * TS);
+    float4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s01 = f4c(v[0], e) + f4c(v[1], e), s23 = f4c(v[2], e) + f4c(v[3], e);
+      const float s45 = f4c(v[4], e) + f4c(v[5], e), s67 = f4c(v[6], e) + f4c(v[7], e);
+      (&o.x)[e] = (s01 + s23) + (s45 + s67);
+    }
+    *reinterpret_cast<float4*>(Pt + r * CP + c4) = o;
+  }
+  __syncthreads();
+  {
+    const float* cr = Pt + rr * CP;
+    float hn[2], cn[2], sn[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float gi = cr[0 + u0 + q] + ((&ta[0].x)[q] + (&xa[0].x)[q]);
+      const float gf = cr[16 + u0 + q] + ((&ta[1].x)[q] + (&xa[1].x)[q]);
+      const float gg = cr[32 + u0 + q] + ((&ta[2].x)[q] + (&xa[2].x)[q]);
+      const float go = cr[48 + u0 + q] + ((&ta[3].x)[q] + (&xa[3].x)[q]);
+      const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+      cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
+      const float tc = tanhf(cn[q]);
+      hn[q] = o_ * tc;
+      sn[q] = sigmoidf_((&sa.x)[q] + (&sb.x)[q]) * tc;
+    }
+    *reinterpret_cast<float2*>(Hs + rr * 16 + u0) = make_float2(hn[0], hn[1]);
+    *reinterpret_cast<float2*>(Ss + rr * 16 + u0) = make_float2(sn[0], sn[1]);
+    if (m < B) {
+      *reinterpret_cast<float2*>(c_out + (int64_t)m * H + j) = make_float2(cn[0], cn[1]);
+      *reinterpret_cast<float2*>(h_out + (int64_t)m * H + j) = make_float2(hn[0], hn[1]);
+      *reinterpret_cast<float2*>(s_out + (int64_t)m * H + j) = make_float2(sn[0], sn[1]);
+      if (hsp_out) {
+        // next step's A fragments: k = j.. in chunk nt, lane (m % 32) + 32 * (u0 / 8), elements u0 % 8..
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 p0, p1, p2;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          __bf16 x0, x1, x2;
+          split3(hn[q], x0, x1, x2);
+          p0[q] = x0; p1[q] = x1; p2[q] = x2;
+        }
+        bf16x8* o = hsp_out + ((size_t)((m >> 5) * KC + nt) * 3) * 64 + (m & 31) + 32 * (u0 >> 3);
+        const int e = u0 & 7;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e) = p0;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e) = p1;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e) = p2;
+      }
+    }
+  }
+  __syncthreads();
+  // partial projections, four outputs j = 4 jq .. 4 jq + 3 of one row per task (float4 store):
+  // part[row][tile][j] = sum_{u < 16} (j < 49 ? h'_u : s_u) W[j][u], fma chain in u order
+  for (int task = t; task < (MODE == 2 ? 0 : BM * (WSP / 4)); task += 512) {
+    const int r = task / (WSP / 4), jq = task % (WSP / 4);
+    const int mr = m0 + r;
+    if (mr < B) {
+      float4 hv[4], sv[4];
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        hv[u4] = *reinterpret_cast<const float4*>(Hs + r * 16 + 4 * u4);
+        sv[u4] = *reinterpret_cast<const float4*>(Ss + r * 16 + 4 * u4);
+      }
+      float acc4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float4 wv = *reinterpret_cast<const float4*>(Wsl + u * WSP + 4 * jq);
+        const float hu = f4c(hv[u >> 2], u & 3), su = f4c(sv[u >> 2], u & 3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc4[e] = __builtin_fmaf(4 * jq + e < P ? hu : su, f4c(wv, e), acc4[e]);
+      }
+      *reinterpret_cast<float4*>(part + ((int64_t)mr * NTn + nt) * PART + 4 * jq) =
+          make_float4(acc4[0], acc4[1], acc4[2], acc4[3]);
+    }
+  }
+}
+// VARIANTS END
+}  // namespace aa
+
 extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, int T, const char* which, int reps,
                        float* out_us) {
   Layout L;
@@ -41,6 +258,24 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
     } else if (!strcmp(which, "enc_v3")) {
       const int M = B * P;
       hipLaunchKernelGGL(k_enc_v3, dim3(((M + EV_BM - 1) / EV_BM) * (H / EV_BN)), dim3(256), 0, s, feats, B, L.C, H, p.enc_w3, p.enc_a_b, w.V);
+    // VARIANT LAUNCH BEGIN
+    } else if (!strcmp(which, "ls_m0")) {
+      auto kern = kv_ls<0>;
+      hipLaunchKernelGGL(kern, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "ls_m1")) {
+      auto kern = kv_ls<1>;
+      hipLaunchKernelGGL(kern, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "ls_m2")) {
+      auto kern = kv_ls<2>;
+      hipLaunchKernelGGL(kern, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "ls_m3")) {
+      auto kern = kv_ls<3>;
+      hipLaunchKernelGGL(kern, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    // VARIANT LAUNCH END
     } else {
       return false;
     }
