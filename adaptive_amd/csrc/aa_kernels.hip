@@ -669,28 +669,29 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
     }
   }
   __syncthreads();
-  // partial projections, four outputs j = 4 jq .. 4 jq + 3 of one row per task (float4 store):
-  // part[row][tile][j] = sum_{u < 16} (j < 49 ? h'_u : s_u) W[j][u], fma chain in u order
-  for (int task = t; task < BM * (WSP / 4); task += 512) {
-    const int r = task / (WSP / 4), jq = task % (WSP / 4);
-    const int mr = m0 + r;
-    if (mr < B) {
-      float4 hv[4], sv[4];
+  // partial projections on fp32 MFMA: part[row][tile][j] = sum_{u < 16} (j < 49 ? h'_u : s_u) W[j][u]
+  // (v_mfma_f32_32x32x2f32, units (i, 8 + i) per instruction, i = 0..7 in order).  Wave -> one
+  // 32x32 block: rows rb*32.., columns cb = 0, 1: W_g j = 0..63; cb = 2, 3: W_s j = 0..63.
+  {
+    const int rb = wave & 1, cb = wave >> 1, li = lane & 31, lh = lane >> 5;
+    const float* X = cb < 2 ? Hs : Ss;
+    const int jj = (cb & 1) * 32 + li, jg = (cb < 2 ? 0 : P) + jj, jgc = jg < WSP ? jg : WSP - 1;
+    floatx16 pacc;
 #pragma unroll
-      for (int u4 = 0; u4 < 4; ++u4) {
-        hv[u4] = *reinterpret_cast<const float4*>(Hs + r * 16 + 4 * u4);
-        sv[u4] = *reinterpret_cast<const float4*>(Ss + r * 16 + 4 * u4);
+    for (int r = 0; r < 16; ++r) pacc[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int u = i + 8 * lh;
+      const float av = X[(rb * 32 + li) * 16 + u];
+      const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
+      pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
+    }
+    if (jj < P) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mr = m0 + rb * 32 + acc_row(r, lane);
+        if (mr < B) part[((int64_t)mr * NTn + nt) * PART + jg] = pacc[r];
       }
-      float acc4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const float4 wv = *reinterpret_cast<const float4*>(Wsl + u * WSP + 4 * jq);
-        const float hu = f4c(hv[u >> 2], u & 3), su = f4c(sv[u >> 2], u & 3);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc4[e] = __builtin_fmaf(4 * jq + e < P ? hu : su, f4c(wv, e), acc4[e]);
-      }
-      *reinterpret_cast<float4*>(part + ((int64_t)mr * NTn + nt) * PART + 4 * jq) =
-          make_float4(acc4[0], acc4[1], acc4[2], acc4[3]);
     }
   }
 }

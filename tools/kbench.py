@@ -33,11 +33,19 @@ def main():
     lib.kb_time.argtypes = [ctypes.POINTER(_lib.Model), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                             ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
     m = model._model_struct()
+    rounds = int(os.environ.get("KB_ROUNDS", "5"))
+    res = {n: [] for n in names}
+    for _ in range(rounds):  # interleaved rounds: variants see the same clocks / cache states
+        for n in names:
+            out = ctypes.c_float()
+            reps = 20 if n.startswith("enc") else 200
+            rc = lib.kb_time(m, feats.data_ptr(), model._ws.data_ptr(), B, T, n.encode(), reps, ctypes.byref(out))
+            if rc:
+                print(f"{n}: rc={rc}", flush=True)
+            res[n].append(out.value)
     for n in names:
-        out = ctypes.c_float()
-        reps = 20 if n.startswith("enc") else 200
-        rc = lib.kb_time(m, feats.data_ptr(), model._ws.data_ptr(), B, T, n.encode(), reps, ctypes.byref(out))
-        print(f"{n:24s} rc={rc} {out.value:9.2f} us", flush=True)
+        v = sorted(res[n])
+        print(f"{n:24s} median {v[len(v) // 2]:8.2f} us  min {v[0]:8.2f}  max {v[-1]:8.2f}", flush=True)
 
 
 if __name__ == "__main__":
