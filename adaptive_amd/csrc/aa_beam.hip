@@ -215,6 +215,19 @@ __device__ __forceinline__ void lse_bfly(float (&m)[16], float (&s)[16], int li)
   }
 }
 
+// transposing butterfly step for a plain reduction (OP 0: max, 1: sum) of 16 rows over 32 lanes
+template <int M, int OP>
+__device__ __forceinline__ void red_bfly(float (&v)[16], int li) {
+  const bool hi = (li & M) != 0;
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    const float sd = hi ? v[k] : v[k + M / 2];
+    const float kp = hi ? v[k + M / 2] : v[k];
+    const float rv = __uint_as_float(partner<M>(__float_as_uint(sd)));
+    v[k] = OP == 0 ? fmaxf(kp, rv) : kp + rv;
+  }
+}
+
 template <int H>
 __global__ __launch_bounds__(256, 2) void k_vbeam3(int R, int V, int Vp, const bf16x8* __restrict__ ua3,
                                                    const bf16x8* __restrict__ w3, const float* __restrict__ bias,
@@ -326,6 +339,145 @@ __global__ __launch_bounds__(256, 2) void k_vbeam3(int R, int V, int Vp, const b
   const int rr = (li >> 1) & 15;
   const int row = m0 + wm * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
   if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wn_ * 32) / 32] = make_float2(fm, fs);
+}
+
+// k_vbeam4: the same logits and summaries as k_vbeam3 from a 128x128 tile whose operand fragments
+// are staged once per workgroup in LDS by global_load_lds (16 B per lane: one wave instruction
+// moves one 1-KB fragment, so the LDS image is the fragment-order image itself) and shared by the
+// four waves (each owns a 64x64 quadrant over the whole K: no partial-tile reduction).  Three
+// stage buffers of one k16 chunk (A: 4 row blocks x 3 planes, W: 4 column blocks x 3 planes =
+// 24 KB); chunk k + 2 is in flight while chunk k is multiplied (counted vmcnt, raw s_barrier).
+constexpr int VB4_NBUF = 3;
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_vbeam4(int R, int V, int Vp, const bf16x8* __restrict__ ua3,
+                                                   const bf16x8* __restrict__ w3, const float* __restrict__ bias,
+                                                   float* __restrict__ logits, float2* __restrict__ gsum) {
+  constexpr int KC = H / 16;
+  __shared__ __attribute__((aligned(16))) bf16x8 stg[VB4_NBUF][24 * 64];
+  const int NG = Vp / 32, NTs = Vp / 128, MT = (R + 127) / 128;
+  const int RB = (R + 63) / 64 * 2;  // row blocks present in ua3 (64-row padded)
+  const int L = xcd_remap(blockIdx.x, MT * NTs);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 31, lh = lane >> 5, wr = wave >> 1, wc = wave & 1;
+  const int m0 = mt * 128, n0 = nt * 128;
+  // this wave's 6 fragments of every chunk: f = 6 wave + i; f < 12: A (row block f / 3, plane f % 3)
+  const bf16x8* src[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = 6 * wave + i;
+    if (f < 12) {
+      int rb = m0 / 32 + f / 3;
+      rb = rb < RB ? rb : RB - 1;
+      src[i] = ua3 + ((size_t)rb * KC * 3 + f % 3) * 64 + lane;
+    } else {
+      const int cb = n0 / 32 + (f - 12) / 3;
+      src[i] = w3 + ((size_t)cb * KC * 3 + (f - 12) % 3) * 64 + lane;
+    }
+  }
+  auto issue = [&](int kc, int buf) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)kc * 3 * 64),
+                                       (__attribute__((address_space(3))) void*)(&stg[buf][(6 * wave + i) * 64]),
+                                       16, 0, 0);
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  // fragments of chunk k are read from LDS while the MFMAs of chunk k - 1 run (two register sets);
+  // chunk k + 2 is in flight meanwhile, so a buffer is refilled right after its last reader passed
+  // the barrier
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [set][block][plane]
+  auto lread = [&](int kc, int set) {
+    const bf16x8* sb = stg[kc % VB4_NBUF];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        fa[set][a][q] = sb[((2 * wr + a) * 3 + q) * 64 + lane];
+        fw[set][a][q] = sb[(12 + (2 * wc + a) * 3 + q) * 64 + lane];
+      }
+  };
+  issue(0, 0);
+  if (KC > 1) issue(1, 1);
+  if (KC > 2) issue(2, 2);
+  if (KC > 2)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (KC > 1)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  lread(0, 0);
+#pragma unroll 2
+  for (int kc = 0; kc < KC; ++kc) {
+    const int set = kc & 1;
+    if (kc + 1 < KC) {
+      if (kc + 2 < KC)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // chunk kc + 1 landed everywhere; chunk kc's buffer is free
+      if (kc + 3 < KC) issue(kc + 3, (kc + 3) % VB4_NBUF);
+      lread(kc + 1, set ^ 1);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[set][a], fw[set][c]);
+    // interleave: 2 MFMAs, then one of the 12 fragment reads of the next chunk
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // epilogue per 32x32 block: logits (+ bias) and the granule's (max, sum exp(x - max)): the row
+  // max by a transposing max-butterfly, broadcast back to the row's 32 lanes, one expf per
+  // element, and the sums by a transposing add-butterfly (fixed pattern: deterministic)
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = n0 + wc * 64 + c * 32 + li;
+    const bool valid = col < V;
+    const float bv = bias[col];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      float x[16], m[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[r] = acc[a][c][r] + bv;
+        const int row = m0 + wr * 64 + a * 32 + acc_row(r, lane);
+        if (row < R) logits[(int64_t)row * Vp + col] = x[r];
+        x[r] = valid ? x[r] : -INFINITY;
+        m[r] = x[r];
+      }
+      red_bfly<16, 0>(m, li);
+      red_bfly<8, 0>(m, li);
+      red_bfly<4, 0>(m, li);
+      red_bfly<2, 0>(m, li);
+      const float gmax = fmaxf(m[0], __uint_as_float(partner<1>(__float_as_uint(m[0]))));
+      // lane pair (2 rr, 2 rr + 1) of half lh now holds the max of row rr of that half
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float g = __shfl(gmax, 2 * r + 32 * lh, 64);
+        m[r] = valid ? expf(x[r] - g) : 0.f;
+      }
+      red_bfly<16, 1>(m, li);
+      red_bfly<8, 1>(m, li);
+      red_bfly<4, 1>(m, li);
+      red_bfly<2, 1>(m, li);
+      const float gs = m[0] + __uint_as_float(partner<1>(__float_as_uint(m[0])));
+      const int rr = (li >> 1) & 15;
+      const int row = m0 + wr * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = make_float2(gmax, gs);
+    }
+  }
 }
 
 // Selection from the granule summaries: one wave per row (K waves per image).  Row log-sum-exp
@@ -561,8 +713,8 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
                          w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {
 #define AA_VB3(H_)                                                                                            \
-  hipLaunchKernelGGL(k_vbeam3<H_>, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, L.V, L.Vp, w.u3, p.mlp_w3, p.mlp_b, \
-                     w.logits, w.gsum)
+  hipLaunchKernelGGL(k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, L.Vp, w.u3,  \
+                     p.mlp_w3, p.mlp_b, w.logits, w.gsum)
       switch (H) {
         case 256: AA_VB3(256); break;
         case 512: AA_VB3(512); break;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over a short bench run (each pass its own rocprofv3 process; --kernel-trace/--stats only).
-# usage: bash tools/pmc.sh <tag> [pass...]   passes: sq mfma fetch write lds
+# usage: [PMC_CMD='python3 prog.py args'] bash tools/pmc.sh <tag> [pass...]   passes: sq mfma fetch write lds l2
 set -u
 tag=${1:-run}; shift
 passes=${@:-sq fetch write}
@@ -17,7 +17,7 @@ for p in $passes; do
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/pmc_$tag/$p -o run -- \
-     python3 bench.py --no-cpu-baseline --no-trace --steps 2 --warmup 1 > gpurun_out/pmc_$tag/$p.log 2>&1
+     ${PMC_CMD:-python3 bench.py --no-cpu-baseline --no-trace --steps 2 --warmup 1} > gpurun_out/pmc_$tag/$p.log 2>&1
   rc=$?; echo "[pmc $p] exit $rc"
   if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmc_$tag/$p.log; exit $rc; fi
 done
