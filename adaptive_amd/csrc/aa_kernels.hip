@@ -494,17 +494,18 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
                                               float* __restrict__ s_out, float* __restrict__ part) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
   constexpr int WSP = 100;  // 98 projection outputs padded to whole float4s
-  __shared__ __attribute__((aligned(16))) float lds[8 * TS + 2 * 64 * 16 + 16 * WSP];
+  constexpr int HP = 68;    // pitch of the transposed h' / s tiles [unit][row]: conflict-free MFMA A reads
+  __shared__ __attribute__((aligned(16))) float lds[4 * TS + 2 * 16 * HP + 16 * WSP];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m0 = mt * BM;
-  float* Pt = lds;                 // [8][64][CP] partial tiles; slot 0 becomes the summed tile
-  float* Hs = Pt + 8 * TS;         // [64][16] h' of the tile
-  float* Ss = Hs + 64 * 16;        // [64][16] s of the tile
-  float* Wsl = Ss + 64 * 16;       // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
+  float* Pt = lds;                 // [4][64][CP] partial tiles; slot 0 becomes the summed tile
+  float* Hs = Pt + 4 * TS;         // [16][HP] h' of the tile, transposed
+  float* Ss = Hs + 16 * HP;        // [16][HP] s of the tile, transposed
+  float* Wsl = Ss + 16 * HP;       // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
 
   // cell-epilogue mapping: thread -> row rr, units u0, u0 + 1 of the tile
   const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
@@ -591,15 +592,30 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // ---- partial tiles -> LDS, fixed-tree sum into slot 0 ----
+  // ---- partial tiles -> LDS in two rounds (4 slots): waves 4..7 store, waves 0..3 add theirs in
+  // registers and store p_w + p_(w+4); then the fixed tree ((q0 + q1) + (q2 + q3)) into slot 0 ----
   {
-    float* dst = Pt + wave * TS;
+    float* dst = Pt + (wave & 3) * TS;
+    if (wave >= 4) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dst[(a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31)] = acc[a][c][r];
+          for (int r = 0; r < 16; ++r) dst[(a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31)] = acc[a][c][r];
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float* e = dst + (a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31);
+            *e = acc[a][c][r] + *e;
+          }
+    }
   }
   {  // transpose the W_g / W_s slice to [unit][j] (j = 98, 99 are zero)
     const int jj = t >> 2, uq = (t & 3) * 4;
@@ -616,16 +632,12 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
   for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
     const int q = t + 512 * i, r = q >> 4, c4 = (q & 15) * 4;
     const float* sp = Pt + r * CP + c4;
-    float4 v[8];
+    float4 v[4];
 #pragma unroll
-    for (int w = 0; w < 8; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
+    for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
     float4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float s01 = f4c(v[0], e) + f4c(v[1], e), s23 = f4c(v[2], e) + f4c(v[3], e);
-      const float s45 = f4c(v[4], e) + f4c(v[5], e), s67 = f4c(v[6], e) + f4c(v[7], e);
-      (&o.x)[e] = (s01 + s23) + (s45 + s67);
-    }
+    for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
     *reinterpret_cast<float4*>(Pt + r * CP + c4) = o;
   }
   __syncthreads();
@@ -644,8 +656,10 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
       hn[q] = o_ * tc;
       sn[q] = sigmoidf_((&sa.x)[q] + (&sb.x)[q]) * tc;
     }
-    *reinterpret_cast<float2*>(Hs + rr * 16 + u0) = make_float2(hn[0], hn[1]);
-    *reinterpret_cast<float2*>(Ss + rr * 16 + u0) = make_float2(sn[0], sn[1]);
+    Hs[u0 * HP + rr] = hn[0];
+    Hs[(u0 + 1) * HP + rr] = hn[1];
+    Ss[u0 * HP + rr] = sn[0];
+    Ss[(u0 + 1) * HP + rr] = sn[1];
     if (m < B) {
       *reinterpret_cast<float2*>(c_out + (int64_t)m * H + j) = make_float2(cn[0], cn[1]);
       *reinterpret_cast<float2*>(h_out + (int64_t)m * H + j) = make_float2(hn[0], hn[1]);
@@ -682,7 +696,7 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int u = i + 8 * lh;
-      const float av = X[(rb * 32 + li) * 16 + u];
+      const float av = X[u * HP + rb * 32 + li];
       const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
       pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
     }

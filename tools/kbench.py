@@ -28,10 +28,14 @@ def main():
     feats = synthetic_features(B, dev, seed=0)
     model.sampler(feats, max_len=T, graph=False)
     torch.cuda.synchronize()
-    lib = ctypes.CDLL(SO)
-    lib.kb_time.restype = ctypes.c_int
-    lib.kb_time.argtypes = [ctypes.POINTER(_lib.Model), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                            ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+    libs = {}
+    for key, path in (("", SO), ("old:", os.environ.get("KB_SO_OLD", ""))):  # "old:<name>" -> a second build
+        if path:
+            lb = ctypes.CDLL(path)
+            lb.kb_time.restype = ctypes.c_int
+            lb.kb_time.argtypes = [ctypes.POINTER(_lib.Model), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+            libs[key] = lb
     m = model._model_struct()
     rounds = int(os.environ.get("KB_ROUNDS", "5"))
     res = {n: [] for n in names}
@@ -39,7 +43,8 @@ def main():
         for n in names:
             out = ctypes.c_float()
             reps = 20 if n.startswith("enc") else 200
-            rc = lib.kb_time(m, feats.data_ptr(), model._ws.data_ptr(), B, T, n.encode(), reps, ctypes.byref(out))
+            lib, kn = (libs["old:"], n[4:]) if n.startswith("old:") else (libs[""], n)
+            rc = lib.kb_time(m, feats.data_ptr(), model._ws.data_ptr(), B, T, kn.encode(), reps, ctypes.byref(out))
             if rc:
                 print(f"{n}: rc={rc}", flush=True)
             res[n].append(out.value)
