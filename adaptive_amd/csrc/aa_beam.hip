@@ -187,34 +187,8 @@ __global__ __launch_bounds__(256) void k_beam_final(int K, int T, int R, const i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Default vocab stage: bf16x3 MFMA logits (fp32-accurate, as the encoder / LSTM GEMMs) over a 64x64
-// tile per workgroup; each wave runs the whole tile over a quarter of K (2-stage register ring of
-// fragment loads), the four partial tiles meet in LDS in a fixed order; epilogue per 32x32 block:
-// logits (+ bias) -> HBM, and per (row, 32-column granule) the pair (max, sum exp(x - max)) by a
-// transposing butterfly over the granule's 32 lanes with the online-softmax merge.
+// Default vocab stage (k_vbeam4 below): bf16x3 MFMA logits and per-granule log-sum-exp summaries.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
-  const float M = fmaxf(m, m2);
-  const float a = m == -INFINITY ? 0.f : s * expf(m - M);
-  const float b = m2 == -INFINITY ? 0.f : s2 * expf(m2 - M);
-  m = M;
-  s = a + b;
-}
-template <int M>
-__device__ __forceinline__ void lse_bfly(float (&m)[16], float (&s)[16], int li) {
-  const bool hi = (li & M) != 0;
-#pragma unroll
-  for (int k = 0; k < M / 2; ++k) {
-    const float sm = hi ? m[k] : m[k + M / 2], ss = hi ? s[k] : s[k + M / 2];
-    float km = hi ? m[k + M / 2] : m[k], ks = hi ? s[k + M / 2] : s[k];
-    const float rm = __uint_as_float(partner<M>(__float_as_uint(sm)));
-    const float rs = __uint_as_float(partner<M>(__float_as_uint(ss)));
-    lse_merge(km, ks, rm, rs);
-    m[k] = km;
-    s[k] = ks;
-  }
-}
-
 // transposing butterfly step for a plain reduction (OP 0: max, 1: sum) of 16 rows over 32 lanes
 template <int M, int OP>
 __device__ __forceinline__ void red_bfly(float (&v)[16], int li) {
@@ -228,120 +202,8 @@ __device__ __forceinline__ void red_bfly(float (&v)[16], int li) {
   }
 }
 
-template <int H>
-__global__ __launch_bounds__(256, 2) void k_vbeam3(int R, int V, int Vp, const bf16x8* __restrict__ ua3,
-                                                   const bf16x8* __restrict__ w3, const float* __restrict__ bias,
-                                                   float* __restrict__ logits, float2* __restrict__ gsum) {
-  constexpr int KC = H / 16, KW = KC / 4;  // k16 chunks per wave (even)
-  __shared__ __attribute__((aligned(16))) float Pt[2 * SC_PT];
-  const int NG = Vp / 32, NTs = Vp / 64, MT = (R + 63) / 64;
-  const int L = xcd_remap(blockIdx.x, MT * NTs);
-  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int li = lane & 31, lh = lane >> 5;
-  const int m0 = mt * 64, n0 = nt * 64;
-  const int kc0 = wave * KW, last = kc0 + KW - 1;
-  const bf16x8* af0 = ua3 + (size_t)(m0 >> 5) * KC * 3 * 64 + lane;
-  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
-  const bf16x8* wf0 = w3 + (size_t)(n0 >> 5) * KC * 3 * 64 + lane;
-  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
-  auto load = [&](int slot, int kc) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const size_t o = ((size_t)kc * 3 + q) * 64;
-      fa[slot][0][q] = af0[o];
-      fa[slot][1][q] = af1[o];
-      fw[slot][0][q] = wf0[o];
-      fw[slot][1][q] = wf1[o];
-    }
-  };
-  load(0, kc0);
-  load(1, kc0 + 1 < last ? kc0 + 1 : last);
-  const int wm = wave >> 1, wn_ = wave & 1;
-  const int col = n0 + wn_ * 32 + li;
-  const float bv = bias[col];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < KW; i += 2) {
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
-      const int nk = kc0 + i + d + 2;
-      load(d, nk < last ? nk : last);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // partial tiles meet in LDS ([col][row], pitch 68): ((p0 + p2) + (p1 + p3))
-  auto put = [&](float* dst) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          *reinterpret_cast<float4*>(dst + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh) =
-              make_float4(acc[a][x][4 * r4], acc[a][x][4 * r4 + 1], acc[a][x][4 * r4 + 2], acc[a][x][4 * r4 + 3]);
-  };
-  auto add = [&](const float* src) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const float4 v = *reinterpret_cast<const float4*>(src + (x * 32 + li) * 68 + a * 32 + 8 * r4 + 4 * lh);
-          acc[a][x][4 * r4] += v.x; acc[a][x][4 * r4 + 1] += v.y;
-          acc[a][x][4 * r4 + 2] += v.z; acc[a][x][4 * r4 + 3] += v.w;
-        }
-  };
-  if (wave >= 2) put(Pt + (wave - 2) * SC_PT);
-  __syncthreads();
-  if (wave < 2) add(Pt + wave * SC_PT);
-  __syncthreads();
-  if (wave == 1) put(Pt);
-  __syncthreads();
-  if (wave == 0) {
-    add(Pt);
-    put(Pt);
-  }
-  __syncthreads();
-  float m[16], sm[16];
-  const bool valid = col < V;
-#pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4) {
-    const float4 v = *reinterpret_cast<const float4*>(Pt + (wn_ * 32 + li) * 68 + wm * 32 + 8 * r4 + 4 * lh);
-    m[4 * r4] = v.x + bv; m[4 * r4 + 1] = v.y + bv; m[4 * r4 + 2] = v.z + bv; m[4 * r4 + 3] = v.w + bv;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wm * 32 + acc_row(r, lane);
-    if (row < R) logits[(int64_t)row * Vp + col] = m[r];
-    sm[r] = valid ? 1.f : 0.f;
-    m[r] = valid ? m[r] : -INFINITY;
-  }
-  lse_bfly<16>(m, sm, li);
-  lse_bfly<8>(m, sm, li);
-  lse_bfly<4>(m, sm, li);
-  lse_bfly<2>(m, sm, li);
-  float fm = m[0], fs = sm[0];
-  lse_merge(fm, fs, __uint_as_float(partner<1>(__float_as_uint(m[0]))), __uint_as_float(partner<1>(__float_as_uint(sm[0]))));
-  const int rr = (li >> 1) & 15;
-  const int row = m0 + wm * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-  if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wn_ * 32) / 32] = make_float2(fm, fs);
-}
-
-// k_vbeam4: the same logits and summaries as k_vbeam3 from a 128x128 tile whose operand fragments
+// k_vbeam4: logits (+ bias) and per (row, 32-column granule) (max, sum exp(x - max)), bf16x3 MFMA
+// (fp32-accurate, as the encoder / LSTM GEMMs), from a 128x128 tile whose operand fragments
 // are staged once per workgroup in LDS by global_load_lds (16 B per lane: one wave instruction
 // moves one 1-KB fragment, so the LDS image is the fragment-order image itself) and shared by the
 // four waves (each owns a 64x64 quadrant over the whole K: no partial-tile reduction).  Three
