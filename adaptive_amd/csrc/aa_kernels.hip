@@ -594,15 +594,20 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
   }
   // ---- partial tiles -> LDS in two rounds (4 slots): waves 4..7 store, waves 0..3 add theirs in
   // registers and store p_w + p_(w+4); then the fixed tree ((q0 + q1) + (q2 + q3)) into slot 0 ----
+  // (tiles stored transposed, [column][row] with pitch CP: a lane's 4 consecutive accumulator rows
+  //  are one 16-B LDS access, conflict-free at pitch 68)
   {
     float* dst = Pt + (wave & 3) * TS;
+    const int li = lane & 31, lh = lane >> 5;
     if (wave >= 4) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) dst[(a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31)] = acc[a][c][r];
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh) =
+                make_float4(acc[a][c][4 * r4], acc[a][c][4 * r4 + 1], acc[a][c][4 * r4 + 2], acc[a][c][4 * r4 + 3]);
     }
     __syncthreads();
     if (wave < 4) {
@@ -611,9 +616,11 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float* e = dst + (a * 32 + acc_row(r, lane)) * CP + c * 32 + (lane & 31);
-            *e = acc[a][c][r] + *e;
+          for (int r4 = 0; r4 < 4; ++r4) {
+            float4* e = reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh);
+            const float4 v = *e;
+            *e = make_float4(acc[a][c][4 * r4] + v.x, acc[a][c][4 * r4 + 1] + v.y, acc[a][c][4 * r4 + 2] + v.z,
+                             acc[a][c][4 * r4 + 3] + v.w);
           }
     }
   }
@@ -630,26 +637,26 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
-    const int q = t + 512 * i, r = q >> 4, c4 = (q & 15) * 4;
-    const float* sp = Pt + r * CP + c4;
+    const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
+    const float* sp = Pt + cq * CP + r4;
     float4 v[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
     float4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
-    *reinterpret_cast<float4*>(Pt + r * CP + c4) = o;
+    *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
   }
   __syncthreads();
   {
-    const float* cr = Pt + rr * CP;
+    const float* cr = Pt + rr;  // column j of the summed tile at cr[j * CP]
     float hn[2], cn[2], sn[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const float gi = cr[0 + u0 + q] + ((&ta[0].x)[q] + (&xa[0].x)[q]);
-      const float gf = cr[16 + u0 + q] + ((&ta[1].x)[q] + (&xa[1].x)[q]);
-      const float gg = cr[32 + u0 + q] + ((&ta[2].x)[q] + (&xa[2].x)[q]);
-      const float go = cr[48 + u0 + q] + ((&ta[3].x)[q] + (&xa[3].x)[q]);
+      const float gi = cr[(0 + u0 + q) * CP] + ((&ta[0].x)[q] + (&xa[0].x)[q]);
+      const float gf = cr[(16 + u0 + q) * CP] + ((&ta[1].x)[q] + (&xa[1].x)[q]);
+      const float gg = cr[(32 + u0 + q) * CP] + ((&ta[2].x)[q] + (&xa[2].x)[q]);
+      const float go = cr[(48 + u0 + q) * CP] + ((&ta[3].x)[q] + (&xa[3].x)[q]);
       const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
       cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
       const float tc = tanhf(cn[q]);
