@@ -15,9 +15,10 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
+DECODE_FUSED_LSTM = 4
 MAX_LANES = 8
 MAX_BEAM = 8
 
@@ -65,7 +66,7 @@ TRACE_ENCODER_KERNELS = 5  # k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM
 
 class Trace(Structure):
     _fields_ = [("encoder_events", c_void_p), ("lstm_events", c_void_p), ("atten_events", c_void_p),
-                ("screen_events", c_void_p), ("rescore_events", c_void_p)]
+                ("screen_events", c_void_p), ("rescore_events", c_void_p), ("gemm_events", c_void_p)]
 
 
 # name -> (restype, argtypes); mirrors include/adaptive_amd.h one to one
@@ -84,6 +85,8 @@ SIGNATURES = {
     "aa_decode_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
     "aa_greedy_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_size_t, POINTER(Trace), c_int32, c_void_p]),
+    "aa_greedy_decode_aux": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, POINTER(Trace), c_int32, c_void_p, c_void_p]),
     "aa_greedy_decode_lanes": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_size_t, POINTER(Trace), c_int32, c_void_p, POINTER(c_void_p),
                                        c_int32]),

@@ -215,6 +215,11 @@ class Encoder2Decoder(nn.Module):
         self.decode_lanes = 1  # HIP streams the greedy step loop is split over (sampler(lanes=...))
         self.fp32_encoder = False  # True: V GEMM on fp32 MFMA instead of the fp32-accurate bf16x3 split
         self.decode_graph = True  # replay repeated sampler calls from a captured hipGraph (aa_decode_plan)
+        # True: split each LSTM step into k_lstm_gemm (on a side stream, overlapping the previous
+        # step's attention / vocab stages) + k_lstm_cell -- same results, but measured slower than the
+        # one-launch k_lstm at B = 512 (cross-stream hand-offs cost more than the overlap gains;
+        # DESIGN.md §4), so off by default
+        self.split_lstm = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -331,7 +336,8 @@ class Encoder2Decoder(nn.Module):
         n = int(self.decode_lanes if lanes is None else lanes)
         if not 1 <= n <= _lib.MAX_LANES:
             raise ValueError(f"lanes must be in [1, {_lib.MAX_LANES}], got {n}")
-        flags = (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
+        flags = ((_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
+                 | self._lstm_flags())
         use_graph = self.decode_graph if graph is None else bool(graph)
         if use_graph and trace is None and B > 0 and T > 0:
             # A plan binds the images pointer; it is captured the second time a key is seen, so
@@ -356,9 +362,13 @@ class Encoder2Decoder(nn.Module):
         ws = self._workspace(lib.aa_decode_workspace_bytes(self._c_dims(), B, T), dev)
         with torch.cuda.device(dev):
             if n == 1:
-                rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                          beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                          trace, flags, _lib.stream_handle())
+                # second stream: the encoder's a_g branch and the next step's h W_hh^T run beside the chain
+                aux = self._aux_stream(dev)
+                aux.wait_stream(torch.cuda.current_stream())  # (the library forks/joins through events too)
+                rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                              beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                                              trace, flags, _lib.stream_handle(),
+                                              aux.cuda_stream)
             else:
                 handles = (ctypes.c_void_p * n)(*[st.cuda_stream for st in self._lanes(n, dev)])
                 rc = lib.aa_greedy_decode_lanes(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
@@ -399,6 +409,17 @@ class Encoder2Decoder(nn.Module):
                                     _lib.DECODE_EXACT_VOCAB if exact_vocab else 0, _lib.stream_handle())
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores
+
+    def _aux_stream(self, dev) -> torch.cuda.Stream:
+        """The side stream of ``aa_greedy_decode_aux`` on ``dev`` (created once, reused)."""
+        cache = self.__dict__.setdefault("_aux_streams", {})
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        if key not in cache:
+            cache[key] = torch.cuda.Stream(device=dev)
+        return cache[key]
+
+    def _lstm_flags(self) -> int:
+        return 0 if self.split_lstm else _lib.DECODE_FUSED_LSTM
 
     def _lanes(self, n: int, dev) -> list:
         """n side streams on ``dev`` (created once, reused)."""

@@ -480,150 +480,26 @@ __device__ __forceinline__ void x3_step(floatx16& acc, const bf16x8 (&a)[3], con
 
 constexpr int LS_CP = 68;  // k_lstm LDS tile pitch (floats): conflict-free cell reads
 
-// G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
-// fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
-// gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
-template <int H, bool G = false>
-__global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
-                                              const float* __restrict__ table,
-                                              const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
-                                              const float* __restrict__ c_in, const int* __restrict__ par,
-                                              const bf16x8* __restrict__ whh3,
-                                              const float* __restrict__ wgs, float* __restrict__ h_out,
-                                              bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
-                                              float* __restrict__ s_out, float* __restrict__ part) {
-  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
-  constexpr int WSP = 100;  // 98 projection outputs padded to whole float4s
-  constexpr int HP = 68;    // pitch of the transposed h' / s tiles [unit][row]: conflict-free MFMA A reads
-  __shared__ __attribute__((aligned(16))) float lds[4 * TS + 2 * 16 * HP + 16 * WSP];
-  constexpr int NTn = H / 16, KC = H / 16;
-  const int MT = (B + BM - 1) / BM;
-  const int L = xcd_remap(blockIdx.x, MT * NTn);
-  const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
+// Cell epilogue shared by k_lstm (GEMM + cell in one launch) and k_lstm_cell (cell of a GEMM done
+// by k_lstm_gemm): thread -> row rr (0..63) of the tile, units u0, u0 + 1 of tile nt.
+// gate[g][q] = (h W_hh^T)[gate g, unit u0 + q] + (table[tok] + xg) -- the pre-activations;
+// sa + sb = x W_x^T of the sentinel; cprev = c_{t-1}; wsv = this thread's float4 of the tile's
+// W_g / W_s slice.  Writes c', h', s, the next step's split-h fragments, and the tile's partial
+// attention projections part[row][nt][j] = sum_{u in tile} (j < 49 ? h'_u W_g[j][u] : s_u W_s[j-49][u])
+// (v_mfma_f32_32x32x2f32, units (i, 8 + i) per instruction, i = 0..7 in order).
+constexpr int LS_HP = 68;    // pitch of the transposed h' / s tiles [unit][row]: conflict-free MFMA A reads
+constexpr int LS_WSP = 100;  // 98 projection outputs padded to whole float4s
+constexpr int LS_TAIL_FLOATS = 2 * 16 * LS_HP + 16 * LS_WSP;
+template <int H>
+__device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const float (&gate)[4][2], float2 sa, float2 sb,
+                                               float2 cprev, float4 wsv, float* Hs, float* h_out,
+                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                               float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int HP = LS_HP, WSP = LS_WSP, NTn = H / 16, KC = H / 16;
+  float* Ss = Hs + 16 * HP;   // [16][HP] s of the tile, transposed
+  float* Wsl = Ss + 16 * HP;  // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = mt * BM;
-  float* Pt = lds;                 // [4][64][CP] partial tiles; slot 0 becomes the summed tile
-  float* Hs = Pt + 4 * TS;         // [16][HP] h' of the tile, transposed
-  float* Ss = Hs + 16 * HP;        // [16][HP] s of the tile, transposed
-  float* Wsl = Ss + 16 * HP;       // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
-
-  // cell-epilogue mapping: thread -> row rr, units u0, u0 + 1 of the tile
-  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
-  const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
-  const int j = nt * 16 + u0;
-  // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
-  //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
-  int64_t tk = tok[(int64_t)mc * tok_ld];
-
-  // ---- GEMM: this wave's K chunks, loads two chunks ahead ----
-  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
-  const int kc0 = wave * per;
-  const bf16x8* af0;
-  const bf16x8* af1;
-  int pc = mc;  // source row of c (and of h, through the fragments)
-  if constexpr (G) {
-    const int ra0 = m0 + (lane & 31), ra1 = ra0 + 32;
-    const int p0 = par[ra0 < B ? ra0 : B - 1], p1 = par[ra1 < B ? ra1 : B - 1];
-    const int hl = 32 * (lane >> 5);
-    af0 = hsp_in + (size_t)(p0 >> 5) * KC * 3 * 64 + (p0 & 31) + hl;
-    af1 = hsp_in + (size_t)(p1 >> 5) * KC * 3 * 64 + (p1 & 31) + hl;
-    pc = par[mc];
-  } else {
-    af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
-    af1 = af0 + (size_t)KC * 3 * 64;
-  }
-  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
-  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
-  auto load = [&](int slot, int kc) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const size_t o = ((size_t)kc * 3 + q) * 64;
-      fa[slot][0][q] = af0[o];
-      fa[slot][1][q] = af1[o];
-      fw[slot][0][q] = wf0[o];
-      fw[slot][1][q] = wf1[o];
-    }
-  };
-  const int last = kc0 + per - 1;
-  asm volatile("" ::: "memory");
-  load(0, kc0);
-  load(1, kc0 + 1 < last ? kc0 + 1 : last);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
-  float2 ta[4], xa[4], sa, sb, cprev;
-  float4 wsv;
-  {
-    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
-    const int N5 = 5 * H;
-    const float* trow = table + tk * N5;
-    const float* xrow = xg + (int64_t)mc * N5;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
-      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
-    }
-    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
-    sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
-    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
-    // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
-    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
-    wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < per; i += 2) {
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
-      const int nk = kc0 + i + d + 2;
-      load(d, nk < last ? nk : last);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // ---- partial tiles -> LDS in two rounds (4 slots): waves 4..7 store, waves 0..3 add theirs in
-  // registers and store p_w + p_(w+4); then the fixed tree ((q0 + q1) + (q2 + q3)) into slot 0 ----
-  // (tiles stored transposed, [column][row] with pitch CP: a lane's 4 consecutive accumulator rows
-  //  are one 16-B LDS access, conflict-free at pitch 68)
-  {
-    float* dst = Pt + (wave & 3) * TS;
-    const int li = lane & 31, lh = lane >> 5;
-    if (wave >= 4) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4)
-            *reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh) =
-                make_float4(acc[a][c][4 * r4], acc[a][c][4 * r4 + 1], acc[a][c][4 * r4 + 2], acc[a][c][4 * r4 + 3]);
-    }
-    __syncthreads();
-    if (wave < 4) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            float4* e = reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh);
-            const float4 v = *e;
-            *e = make_float4(acc[a][c][4 * r4] + v.x, acc[a][c][4 * r4 + 1] + v.y, acc[a][c][4 * r4 + 2] + v.z,
-                             acc[a][c][4 * r4 + 3] + v.w);
-          }
-    }
-  }
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr, j = nt * 16 + u0;
   {  // transpose the W_g / W_s slice to [unit][j] (j = 98, 99 are zero)
     const int jj = t >> 2, uq = (t & 3) * 4;
     if (t < 2 * P * 4) {
@@ -634,30 +510,12 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
       Wsl[(z >> 1) * WSP + 2 * P + (z & 1)] = 0.f;
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
-    const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
-    const float* sp = Pt + cq * CP + r4;
-    float4 v[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
-    float4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
-    *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
-  }
-  __syncthreads();
   {
-    const float* cr = Pt + rr;  // column j of the summed tile at cr[j * CP]
     float hn[2], cn[2], sn[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const float gi = cr[(0 + u0 + q) * CP] + ((&ta[0].x)[q] + (&xa[0].x)[q]);
-      const float gf = cr[(16 + u0 + q) * CP] + ((&ta[1].x)[q] + (&xa[1].x)[q]);
-      const float gg = cr[(32 + u0 + q) * CP] + ((&ta[2].x)[q] + (&xa[2].x)[q]);
-      const float go = cr[(48 + u0 + q) * CP] + ((&ta[3].x)[q] + (&xa[3].x)[q]);
-      const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+      const float i_ = sigmoidf_(gate[0][q]), f_ = sigmoidf_(gate[1][q]), g_ = tanhf(gate[2][q]),
+                  o_ = sigmoidf_(gate[3][q]);
       cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
       const float tc = tanhf(cn[q]);
       hn[q] = o_ * tc;
@@ -690,9 +548,7 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
     }
   }
   __syncthreads();
-  // partial projections on fp32 MFMA: part[row][tile][j] = sum_{u < 16} (j < 49 ? h'_u : s_u) W[j][u]
-  // (v_mfma_f32_32x32x2f32, units (i, 8 + i) per instruction, i = 0..7 in order).  Wave -> one
-  // 32x32 block: rows rb*32.., columns cb = 0, 1: W_g j = 0..63; cb = 2, 3: W_s j = 0..63.
+  // Wave -> one 32x32 block: rows rb*32.., columns cb = 0, 1: W_g j = 0..63; cb = 2, 3: W_s j = 0..63.
   {
     const int rb = wave & 1, cb = wave >> 1, li = lane & 31, lh = lane >> 5;
     const float* X = cb < 2 ? Hs : Ss;
@@ -715,6 +571,258 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
       }
     }
   }
+}
+
+// GEMM main loop shared by k_lstm and k_lstm_gemm: wave w accumulates the 64x64 tile (2 x 2 blocks
+// of 32x32) over its K chunks [w KC/8, (w+1) KC/8) from fragments af0/af1 (the tile's two 32-row
+// blocks of split h) and wf0/wf1 (its two 32-column blocks of split W_hh), two chunks in flight;
+// then the eight partial tiles are summed in LDS: waves 4..7 store, waves 0..3 add theirs and store
+// q_w = p_w + p_(w+4) into slot w (tiles stored transposed, [column][row] with pitch LS_CP: a lane's
+// 4 consecutive accumulator rows are one 16-B access).  The caller finishes the fixed tree
+// ((q0 + q1) + (q2 + q3)) after a barrier.  `between` runs after the first loads are issued
+// (token-dependent gathers of k_lstm).
+template <int H, class F>
+__device__ __forceinline__ void lstm_gemm_partials(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
+                                                   const bf16x8* wf1, float* Pt, F&& between) {
+  constexpr int KC = H / 16, CP = LS_CP, TS = 64 * LS_CP;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
+  const int kc0 = wave * per;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][0][q] = af0[o];
+      fa[slot][1][q] = af1[o];
+      fw[slot][0][q] = wf0[o];
+      fw[slot][1][q] = wf1[o];
+    }
+  };
+  const int last = kc0 + per - 1;
+  asm volatile("" ::: "memory");
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  between();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < per; i += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
+      const int nk = kc0 + i + d + 2;
+      load(d, nk < last ? nk : last);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* dst = Pt + (wave & 3) * TS;
+  const int li = lane & 31, lh = lane >> 5;
+  if (wave >= 4) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[a][c][4 * r4], acc[a][c][4 * r4 + 1], acc[a][c][4 * r4 + 2], acc[a][c][4 * r4 + 3]);
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          float4* e = reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh);
+          const float4 v = *e;
+          *e = make_float4(acc[a][c][4 * r4] + v.x, acc[a][c][4 * r4 + 1] + v.y, acc[a][c][4 * r4 + 2] + v.z,
+                           acc[a][c][4 * r4 + 3] + v.w);
+        }
+  }
+}
+
+// G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
+// fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
+// gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
+template <int H, bool G = false>
+__global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+                                              const float* __restrict__ table,
+                                              const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
+                                              const float* __restrict__ c_in, const int* __restrict__ par,
+                                              const bf16x8* __restrict__ whh3,
+                                              const float* __restrict__ wgs, float* __restrict__ h_out,
+                                              bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                              float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
+  __shared__ __attribute__((aligned(16))) float lds[4 * TS + LS_TAIL_FLOATS];
+  constexpr int NTn = H / 16, KC = H / 16;
+  const int MT = (B + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63;
+  const int m0 = mt * BM;
+  float* Pt = lds;  // [4][64][CP] partial tiles
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
+  const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
+  const int j = nt * 16 + u0;
+  // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
+  //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
+  int64_t tk = tok[(int64_t)mc * tok_ld];
+  const bf16x8* af0;
+  const bf16x8* af1;
+  int pc = mc;  // source row of c (and of h, through the fragments)
+  if constexpr (G) {
+    const int ra0 = m0 + (lane & 31), ra1 = ra0 + 32;
+    const int p0 = par[ra0 < B ? ra0 : B - 1], p1 = par[ra1 < B ? ra1 : B - 1];
+    const int hl = 32 * (lane >> 5);
+    af0 = hsp_in + (size_t)(p0 >> 5) * KC * 3 * 64 + (p0 & 31) + hl;
+    af1 = hsp_in + (size_t)(p1 >> 5) * KC * 3 * 64 + (p1 & 31) + hl;
+    pc = par[mc];
+  } else {
+    af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+    af1 = af0 + (size_t)KC * 3 * 64;
+  }
+  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
+  float2 ta[4], xa[4], sa, sb, cprev;
+  float4 wsv;
+  lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, [&] {
+    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+    const int N5 = 5 * H;
+    const float* trow = table + tk * N5;
+    const float* xrow = xg + (int64_t)mc * N5;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
+    }
+    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+    sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
+    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
+    // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
+    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+    wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
+  });
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
+    const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
+    const float* sp = Pt + cq * CP + r4;
+    float4 v[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
+    float4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
+    *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
+  }
+  __syncthreads();
+  float gate[4][2];
+  {
+    const float* cr = Pt + rr;  // column j of the summed tile at cr[j * CP]
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
+  }
+  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + 4 * TS, h_out, hsp_out, c_out, s_out, part);
+}
+
+// Split LSTM step, part 1: G = h_{t-1} W_hh^T (the tile sums of k_lstm, same fixed order) written
+// to gates [B][H/16 tiles][8 unit pairs][4 gates][2 units] -- the order k_lstm_cell's threads read
+// (two float4 each).  Depends only on h_{t-1}, so the decode loop runs it on a second stream beside
+// the previous step's attention, vocab screen and rescoring (the token is not needed here).
+template <int H>
+__global__ __launch_bounds__(512) void k_lstm_gemm(int B, const bf16x8* __restrict__ hsp_in,
+                                                   const bf16x8* __restrict__ whh3, float* __restrict__ gates) {
+  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP, NTn = H / 16, KC = H / 16;
+  __shared__ __attribute__((aligned(16))) float Pt[4 * TS];
+  const int MT = (B + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;
+  const int t = threadIdx.x, lane = t & 63;
+  const int m0 = mt * BM;
+  const bf16x8* af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
+  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, [] {});
+  __syncthreads();
+  const int rr = t >> 3, pp = t & 7, m = m0 + rr;
+  float o[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float* sp = Pt + (16 * g + 2 * pp + q) * CP + rr;
+      o[2 * g + q] = (sp[0] + sp[TS]) + (sp[2 * TS] + sp[3 * TS]);
+    }
+  if (m < B) {
+    float4* dst = reinterpret_cast<float4*>(gates + (((int64_t)m * NTn + nt) * 8 + pp) * 8);
+    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+// Split LSTM step, part 2: the cell of k_lstm on G from k_lstm_gemm (bit-identical to k_lstm).
+// G (beam search): row m continues row par[m]: its GEMM row and c come from that row.
+template <int H, bool G = false>
+__global__ __launch_bounds__(512) void k_lstm_cell(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+                                                   const float* __restrict__ table, const float* __restrict__ xg,
+                                                   const float* __restrict__ gates, const float* __restrict__ c_in,
+                                                   const int* __restrict__ par, const float* __restrict__ wgs,
+                                                   float* __restrict__ h_out, bf16x8* __restrict__ hsp_out,
+                                                   float* __restrict__ c_out, float* __restrict__ s_out,
+                                                   float* __restrict__ part) {
+  constexpr int BM = 64, NTn = H / 16;
+  __shared__ __attribute__((aligned(16))) float lds[LS_TAIL_FLOATS];
+  const int MT = (B + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;
+  const int t = threadIdx.x, m0 = mt * BM;
+  const int rr = t >> 3, pp = t & 7, u0 = 2 * pp, m = m0 + rr;
+  const int mc = m < B ? m : B - 1;
+  const int j = nt * 16 + u0;
+  int64_t tk = tok[(int64_t)mc * tok_ld];
+  const int pc = G ? par[mc] : mc;
+  const float4* gsrc = reinterpret_cast<const float4*>(gates + (((int64_t)pc * NTn + nt) * 8 + pp) * 8);
+  const float4 g0 = gsrc[0], g1 = gsrc[1];
+  const float2 cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
+  const float4* wsrc = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+  const float4 wsv = wsrc[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
+  const int N5 = 5 * H;
+  const float* xrow = xg + (int64_t)mc * N5;
+  float2 xa[4], ta[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
+  const float2 sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
+  tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+  const float* trow = table + tk * N5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+  const float2 sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+  const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  float gate[4][2];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) gate[g][q] = gv[2 * g + q] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
+  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds, h_out, hsp_out, c_out, s_out, part);
 }
 
 __global__ void k_fill_tok(int64_t* __restrict__ tok, int B, int64_t v) {
@@ -1667,7 +1775,7 @@ static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
 }
 
 struct DecodeWS {
-  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part;
+  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part, *gates;
   uint16_t* ub;
   bf16x8* hsp[2];
   float4* summ;
@@ -1690,6 +1798,7 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.u = c.take<float>((size_t)B * L.H);
   w.unorm = c.take<float>((size_t)B);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
+  w.gates = c.take<float>((size_t)B * 4 * L.H);  // split LSTM step: h W_hh^T of the next step
   w.ub = c.take<uint16_t>((size_t)((B + 63) / 64) * 64 * L.H);  // fragment order, 64-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
@@ -1714,16 +1823,12 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 }
 
 
-// LSTM + attention for one step (shared by the step API and the greedy loop)
-// par != nullptr: beam search (rows continue rows par[] of the previous step; kdiv rows per image)
-static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld,
-                              const float* V, const float* vwv, const float* xg, const bf16x8* hsp_in,
-                              const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
-                              float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
-                              const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1,
-                              bf16x8* ub3 = nullptr) {
+// LSTM step (GEMM + cell in one launch), shared by the step API, the greedy loop and beam search.
+// par != nullptr: beam search (rows continue rows par[] of the previous step)
+static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
+                        const bf16x8* hsp_in, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
+                        float* s_buf, float* part, hipStream_t s, const int* par = nullptr) {
   const int H = L.H, MT = (B + 63) / 64;
-  rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
 #define AA_LSTM(H_)                                                                                          \
   do {                                                                                                       \
     if (par)                                                                                                 \
@@ -1740,8 +1845,48 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
     default: AA_LSTM(1024); break;
   }
 #undef AA_LSTM
-  rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
-  rec(tr ? tr->atten_events : nullptr, 2 * t, s);
+}
+
+// Split LSTM step, part 1 (k_lstm_gemm): gates = h_{t-1} W_hh^T for all B rows.
+static void lstm_gemm_launch(const Layout& L, const MP& p, int B, const bf16x8* hsp_in, float* gates, hipStream_t s) {
+  const int H = L.H, MT = (B + 63) / 64;
+  switch (H) {
+    case 256: hipLaunchKernelGGL(k_lstm_gemm<256>, dim3(MT * 16), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
+    case 512: hipLaunchKernelGGL(k_lstm_gemm<512>, dim3(MT * 32), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
+    case 768: hipLaunchKernelGGL(k_lstm_gemm<768>, dim3(MT * 48), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
+    default: hipLaunchKernelGGL(k_lstm_gemm<1024>, dim3(MT * 64), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
+  }
+}
+
+// Split LSTM step, part 2 (k_lstm_cell): the cell on the gates of part 1.
+static void lstm_cell_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
+                             const float* gates, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
+                             float* s_buf, float* part, hipStream_t s, const int* par = nullptr) {
+  const int H = L.H, MT = (B + 63) / 64;
+#define AA_CELL(H_)                                                                                           \
+  do {                                                                                                        \
+    if (par)                                                                                                  \
+      hipLaunchKernelGGL((k_lstm_cell<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,  \
+                         p.table, xg, gates, c_in, par, p.wgs, h_out, hsp_out, c_out, s_buf, part);          \
+    else                                                                                                      \
+      hipLaunchKernelGGL((k_lstm_cell<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
+                         p.table, xg, gates, c_in, par, p.wgs, h_out, hsp_out, c_out, s_buf, part);          \
+  } while (0)
+  switch (H) {
+    case 256: AA_CELL(256); break;
+    case 512: AA_CELL(512); break;
+    case 768: AA_CELL(768); break;
+    default: AA_CELL(1024); break;
+  }
+#undef AA_CELL
+}
+
+// Attention for one step (kdiv rows per image: beam search)
+static void atten_launch(const Layout& L, const MP& p, int B, const float* V, const float* vwv, const float* h_out,
+                         float* s_buf, float* part, float* u, uint16_t* ub, float* unorm, float* alpha,
+                         int64_t alpha_ld, float* beta, int64_t beta_ld, hipStream_t s, int kdiv = 1,
+                         bf16x8* ub3 = nullptr) {
+  const int H = L.H;
 #define AA_ATTEN(HPT_)                                                                                     \
   hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
                      alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
@@ -1756,6 +1901,20 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
   }
 #undef AA_ATTEN
 #undef AA_ATTEN5
+}
+
+// LSTM + attention for one step (fused LSTM kernel)
+static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld,
+                              const float* V, const float* vwv, const float* xg, const bf16x8* hsp_in,
+                              const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
+                              float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
+                              const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1,
+                              bf16x8* ub3 = nullptr) {
+  rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
+  lstm_launch(L, p, B, tok, tok_ld, xg, hsp_in, c_in, h_out, hsp_out, c_out, s_buf, part, s, par);
+  rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
+  rec(tr ? tr->atten_events : nullptr, 2 * t, s);
+  atten_launch(L, p, B, V, vwv, h_out, s_buf, part, u, ub, unorm, alpha, alpha_ld, beta, beta_ld, s, kdiv, ub3);
   rec(tr ? tr->atten_events : nullptr, 2 * t + 1, s);
 }
 
@@ -1800,8 +1959,12 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
 
 // The T-step loop over rows [r0, r0 + Bl) of the batch (every workspace array is row-indexed, so a
 // lane is the same loop on offset pointers; keys are [T][B]).
-static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, bool exact,
-                        int64_t* ids, float* alpha, float* beta, const aa_trace* trace, hipStream_t s) {
+// sg != nullptr: split LSTM steps -- k_lstm_gemm for step t+1 (it needs only h_t) runs on sg beside
+// step t's attention, vocab screen and rescoring on s, and k_lstm_cell of step t+1 waits for it
+// (sg == s: the same kernels in stream order).  sg == nullptr: the fused k_lstm.
+static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, bool exact,
+                       int64_t* ids, float* alpha, float* beta, const aa_trace* trace, hipStream_t s,
+                       hipStream_t sg = nullptr) {
   const int H = L.H, MT = (Bl + 63) / 64, NTn = L.Vp / VS_TILE;
   const float* V = w.V + (size_t)r0 * P * H;
   const float* vwv = w.vwv + (size_t)r0 * P * PP;
@@ -1819,15 +1982,54 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
   int64_t* idsl = ids + (size_t)r0 * T;
   float* al = alpha ? alpha + (size_t)r0 * T * P : nullptr;
   float* bl = beta ? beta + (size_t)r0 * T : nullptr;
+  float* gates = w.gates + (size_t)r0 * 4 * H;
+  const bool split = sg != nullptr, two = split && sg != s;
+  aa_event_t* gev = trace ? trace->gemm_events : nullptr;
+  aa_event_t* lev = trace ? trace->lstm_events : nullptr;
+  aa_event_t* aev = trace ? trace->atten_events : nullptr;
+  hipEvent_t ev_h = nullptr, ev_g = nullptr;  // h_t ready (s -> sg), gates ready (sg -> s)
+  auto gemm = [&](int t, hipStream_t gs) {   // gates of step t from h_{t-1} (fragments hs[t & 1])
+    rec(gev, 2 * t, gs);
+    lstm_gemm_launch(L, p, Bl, hs[t & 1], gates, gs);
+    rec(gev, 2 * t + 1, gs);
+  };
+  if (two) {
+    AA_TRY(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
+    AA_TRY(hipEventCreateWithFlags(&ev_g, hipEventDisableTiming));
+    AA_TRY(hipEventRecord(ev_h, s));
+    AA_TRY(hipStreamWaitEvent(sg, ev_h, 0));
+  }
+  if (split) {
+    gemm(0, sg);
+    if (two) AA_TRY(hipEventRecord(ev_g, sg));
+  }
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
     // token of step t-1: ids[:, t-1] (written by the previous step), <start> at t = 0
     const int64_t* tok = t ? idsl + (t - 1) : w.tok0 + r0;
     const int tok_ld = t ? T : 1;
     uint64_t* kt = w.keys + (size_t)t * B + r0;
-    lstm_atten_launch(L, p, Bl, tok, tok_ld, V, vwv, xg, hs[cur], cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, u,
-                      exact ? nullptr : ub, exact ? nullptr : unorm, al ? al + (size_t)t * P : nullptr,
-                      (int64_t)T * P, bl ? bl + t : nullptr, T, trace, t, s);
+    float* alt = al ? al + (size_t)t * P : nullptr;
+    float* blt = bl ? bl + t : nullptr;
+    if (split) {
+      if (two) AA_TRY(hipStreamWaitEvent(s, ev_g, 0));
+      rec(lev, 2 * t, s);
+      lstm_cell_launch(L, p, Bl, tok, tok_ld, xg, gates, cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, s);
+      rec(lev, 2 * t + 1, s);
+      if (two && t + 1 < T) {
+        AA_TRY(hipEventRecord(ev_h, s));
+        AA_TRY(hipStreamWaitEvent(sg, ev_h, 0));
+        gemm(t + 1, sg);
+        AA_TRY(hipEventRecord(ev_g, sg));
+      }
+      rec(aev, 2 * t, s);
+      atten_launch(L, p, Bl, V, vwv, hb[nxt], sb, part, u, exact ? nullptr : ub, exact ? nullptr : unorm, alt,
+                   (int64_t)T * P, blt, T, s);
+      rec(aev, 2 * t + 1, s);
+    } else {
+      lstm_atten_launch(L, p, Bl, tok, tok_ld, V, vwv, xg, hs[cur], cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, u,
+                        exact ? nullptr : ub, exact ? nullptr : unorm, alt, (int64_t)T * P, blt, T, trace, t, s);
+    }
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     rec(sev, 2 * t, s);
@@ -1854,7 +2056,13 @@ static void decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, 
                          idsl, T, t);
       rec(rev, 2 * t + 1, s);
     }
+    if (split && !two && t + 1 < T) gemm(t + 1, s);
   }
+  if (two) {  // every sg launch was waited for by a k_lstm_cell on s
+    AA_TRY(hipEventDestroy(ev_h));
+    AA_TRY(hipEventDestroy(ev_g));
+  }
+  return launch_status();
 }
 
 static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
@@ -1892,7 +2100,10 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
       AA_TRY(hipEventRecord(e, s));
       AA_TRY(hipStreamWaitEvent(ls, e, 0));
     }
-    decode_rows(L, p, w, B, 0, B, T, exact, ids, alpha, beta, trace, ls);
+    // the split LSTM step uses the aux stream (if any) for the GEMM of the next step
+    hipStream_t sg = (flags & AA_DECODE_FUSED_LSTM) || !aux || aux == ls ? nullptr : aux;
+    rc = decode_rows(L, p, w, B, 0, B, T, exact, ids, alpha, beta, trace, ls, sg);
+    if (rc) return rc;
     if (ls != s) {
       AA_TRY(hipEventRecord(e, ls));
       AA_TRY(hipStreamWaitEvent(s, e, 0));
@@ -1909,7 +2120,8 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
       if (r1 > B) r1 = B;
       hipStream_t ls = (hipStream_t)lanes[i];
       AA_TRY(hipStreamWaitEvent(ls, fork, 0));
-      decode_rows(L, p, w, B, r0, r1 - r0, T, exact, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
+      rc = decode_rows(L, p, w, B, r0, r1 - r0, T, exact, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
+      if (rc) return rc;
       AA_TRY(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
       AA_TRY(hipEventRecord(join[i], ls));
     }
@@ -1927,6 +2139,13 @@ int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T
                      aa_stream_t stream) {
   return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
                      nullptr, 0);
+}
+
+int aa_greedy_decode_aux(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
+                         float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                         aa_stream_t stream, aa_stream_t aux_stream) {
+  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
+                     nullptr, 0, (hipStream_t)aux_stream);
 }
 
 int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,

@@ -23,6 +23,7 @@ from .adaptive_attention import ATT, _Plan
 class _Slot:
     def __init__(self, dev):
         self.stream = torch.cuda.Stream(device=dev)
+        self.aux = torch.cuda.Stream(device=dev)  # the slot's side stream (aa_greedy_decode_aux)
         self.ws = None
         self.plans = collections.OrderedDict()  # images key -> _Plan
         self.seen = set()
@@ -68,13 +69,14 @@ class DecodePipeline:
         ready.record()  # images (and any repack) are ready on the caller's stream
         s = slot.stream
         s.wait_event(ready)
+        slot.aux.wait_event(ready)
         images.record_stream(s)
         with torch.cuda.device(dev), torch.cuda.stream(s):
-            key = (images.data_ptr(), B, T, m._packed.data_ptr())
+            key = (images.data_ptr(), B, T, m._packed.data_ptr(), m._lstm_flags())
             plan = slot.plans.get(key) if self.graph else None
             if plan is None and self.graph and key in slot.seen and B > 0 and T > 0:
                 s.synchronize()
-                plan = slot.plans[key] = _Plan(lib, model, images, B, T, 0, 1, m._c_dims(), dev)
+                plan = slot.plans[key] = _Plan(lib, model, images, B, T, m._lstm_flags(), 1, m._c_dims(), dev)
                 while len(slot.plans) > self.MAX_PLANS:
                     slot.plans.popitem(last=False)
             slot.seen.add(key)
@@ -88,9 +90,12 @@ class DecodePipeline:
                 nbytes = lib.aa_decode_workspace_bytes(m._c_dims(), B, T)
                 if nbytes and (slot.ws is None or slot.ws.numel() < nbytes):
                     slot.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                rc = lib.aa_greedy_decode(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                          beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None, 0,
-                                          s.cuda_stream)
+                rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                              beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None,
+                                              m._lstm_flags(), s.cuda_stream,
+                                              # the other slots already fill the chip: one stream per slot
+                                              # unless the LSTM steps are split
+                                              slot.aux.cuda_stream if m.split_lstm else None)
                 _lib.check(rc, "greedy_decode")
                 out = (ids, alpha, beta)
             done = torch.cuda.Event()

@@ -60,7 +60,9 @@ def flops_per_caption(T: int) -> dict:
             # this build: the embedding / v_g parts of the LSTM + sentinel inputs come from the
             # pack-time token table and the once-per-batch x_g GEMM; k_lstm runs h W_hh^T and the
             # attention projections of h and s in its epilogue
-            "xg": 2 * E * 5 * H, "k_lstm": 2 * H * 4 * H + proj, "k_vscreen": vocab}
+            "xg": 2 * E * 5 * H, "k_lstm": 2 * H * 4 * H + proj, "k_vscreen": vocab,
+            # split LSTM step (aa_greedy_decode_aux): the GEMM alone, and the cell with the projections
+            "k_lstm_gemm": 2 * H * 4 * H, "proj": proj}
 
 
 def kernel_costs(B: int, T: int) -> dict:
@@ -74,11 +76,21 @@ def kernel_costs(B: int, T: int) -> dict:
         "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),
         "k_gemm_bias(x_g)": ("mfma", f["xg"] * B),
         "k_lstm": ("mfma_x3", f["k_lstm"] * B),
+        "k_lstm_gemm": ("mfma_x3", f["k_lstm_gemm"] * B),
+        "k_lstm_cell": ("hbm", lstm_cell_bytes(B)),
         "k_atten": ("hbm", atten_bytes_per_row() * B),
         "k_vscreen": ("mfma_bf16", f["k_vscreen"] * B),
         # per row: 320 granule summaries + u + the winning W_m row + id/key out (candidate count varies)
         "k_vrescore": ("hbm", B * ((V + 127) // 128 * 4 * 16 + 4 * H + 4 * H + 16)),
     }
+
+
+def lstm_cell_bytes(B: int) -> int:
+    """k_lstm_cell algorithmic bytes per launch: per row the GEMM gates (4H), the token's table row
+    and the x_g row (5H each), c in; h, c, s out (+ h as 3 bf16 planes) and the H/16 tiles' 98
+    projection partials; per 64-row tile the W_g / W_s slices."""
+    per_row = 4 * (4 * H + 5 * H + 5 * H + H + 3 * H) + 2 * 3 * H + 4 * (H // 16) * 2 * P
+    return B * per_row + ((B + 63) // 64) * 4 * 2 * P * H
 
 
 def atten_bytes_per_row() -> int:
@@ -130,6 +142,8 @@ def main():
     ap.add_argument("--pipeline-depth", type=int, default=2, help="batches in flight in the headline region "
                     "(adaptive_amd.pipeline.DecodePipeline: batch i+1 starts on its own stream while batch i "
                     "finishes); 1 = one sampler() call after another")
+    ap.add_argument("--split-lstm", action="store_true", help="split LSTM steps: k_lstm_gemm on a side stream "
+                    "+ k_lstm_cell instead of the one-launch k_lstm (same results; slower at B=512)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -146,6 +160,7 @@ def main():
 
     B, T = args.batch, args.max_len
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    model.split_lstm = args.split_lstm
     feats = synthetic_features(B, dev, seed=0, row0=rank * B)  # rows [rank*B, (rank+1)*B) of the global batch
     ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
 
@@ -170,9 +185,10 @@ def main():
     traces = []
     if not args.no_trace:
         for _ in range(K):
-            ev = {k: EventArray(2 * T) for k in ("lstm", "atten", "screen", "rescore")}
+            ev = {k: EventArray(2 * T) for k in ("lstm", "atten", "screen", "rescore", "gemm")}
             ev["encoder"] = EventArray(2 * _lib.TRACE_ENCODER_KERNELS)
-            tr = _lib.Trace(ev["encoder"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["screen"].ptr, ev["rescore"].ptr)
+            tr = _lib.Trace(ev["encoder"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["screen"].ptr, ev["rescore"].ptr,
+                            ev["gemm"].ptr if model.split_lstm else None)
             traces.append((ev, tr))
     def timed(trace_list, pipeline=False):
         torch.cuda.synchronize()
@@ -212,13 +228,18 @@ def main():
     kernels = {}
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
+        lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
         per = {k: [] for k in ("k_avgpool", "k_enc_v3", "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)",
-                               "k_lstm", "k_atten", "k_vscreen", "k_vrescore")}
+                               lstm, "k_atten", "k_vscreen", "k_vrescore")}
+        if model.split_lstm:
+            per["k_lstm_gemm"] = []
         for ev, _ in traces:
             enc = ev["encoder"].pair_durations_ms()
             for i, k in enumerate(("k_avgpool", "k_enc_v3", "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)")):
                 per[k].append(enc[i])
-            per["k_lstm"] += ev["lstm"].pair_durations_ms()
+            per[lstm] += ev["lstm"].pair_durations_ms()
+            if model.split_lstm:
+                per["k_lstm_gemm"] += ev["gemm"].pair_durations_ms()
             per["k_atten"] += ev["atten"].pair_durations_ms()
             per["k_vscreen"] += ev["screen"].pair_durations_ms()
             per["k_vrescore"] += ev["rescore"].pair_durations_ms()
@@ -269,7 +290,9 @@ def main():
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
                    "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else ""),
                    "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
-                   "hip_graph": not args.no_graph, "batches_in_flight": depth},
+                   "hip_graph": not args.no_graph, "batches_in_flight": depth,
+                   "lstm_step": "split (k_lstm_gemm on a side stream + k_lstm_cell)" if model.split_lstm
+                   else "fused (k_lstm)"},
         "sequential": {"value": world * B * K / elapsed_seq, "ms_per_step": 1e3 * elapsed_seq / K,
                        "note": "one sampler() call after another (batches_in_flight = 1)"},
         "roofline": roofline,

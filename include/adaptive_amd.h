@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 7
+#define AA_ABI_VERSION 8
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -121,7 +121,10 @@ typedef struct aa_model {
  *   encoder_events: 2*AA_TRACE_ENCODER_KERNELS events, launches in the order
  *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
  *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen
- *                   (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused then). */
+ *                   (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused then);
+ *                   lstm = k_lstm, or k_lstm_cell when the step is split (aa_greedy_decode_aux);
+ *   gemm_events:    2*T events, launch i = k_lstm_gemm of step i (split steps only; recorded on
+ *                   the aux stream). */
 #define AA_TRACE_ENCODER_KERNELS 5
 typedef struct aa_trace {
   aa_event_t* encoder_events;
@@ -129,6 +132,7 @@ typedef struct aa_trace {
   aa_event_t* atten_events;
   aa_event_t* screen_events;
   aa_event_t* rescore_events;
+  aa_event_t* gemm_events;
 } aa_trace;
 
 AA_API int aa_abi_version(void);
@@ -173,6 +177,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 /* Decode flags */
 #define AA_DECODE_EXACT_VOCAB 1 /* compute every fp32 logit (fp32 MFMA GEMM + fused argmax) instead of
                                    the bf16 screen + exact fp32 rescoring; both give the same ids */
+#define AA_DECODE_FUSED_LSTM 4 /* aa_greedy_decode_aux / decode plans: keep the one-launch LSTM step
+                                  (k_lstm) instead of the split k_lstm_gemm + k_lstm_cell */
 #define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of
                                     the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v3) */
 
@@ -188,6 +194,19 @@ AA_API int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, in
                             int64_t* ids, float* alpha, float* beta, void* workspace,
                             size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                             aa_stream_t stream);
+
+/* aa_greedy_decode with a second stream `aux_stream` for work off the step chain: the encoder's
+ * a_g branch (avgpool, heads, x_g GEMM) beside the V branch, and every LSTM step split in two --
+ * k_lstm_gemm (h_{t-1} W_hh^T, which needs no token) for step t+1 runs on aux_stream beside step
+ * t's attention, vocab screen and rescoring on `stream`, then k_lstm_cell of step t+1 (token
+ * gather, cell, sentinel, projections) waits for it.  Same arithmetic in the same order as the
+ * one-launch k_lstm, so the results equal aa_greedy_decode's bit for bit.  Fork/join through
+ * events: the call is complete (and graph-capturable) on `stream`.  aux_stream NULL or equal to
+ * `stream`: aa_greedy_decode.  flags & AA_DECODE_FUSED_LSTM keeps k_lstm. */
+AA_API int aa_greedy_decode_aux(const aa_model* m, const float* feats, int32_t B, int32_t T,
+                                int64_t* ids, float* alpha, float* beta, void* workspace,
+                                size_t workspace_bytes, const aa_trace* trace, int32_t flags,
+                                aa_stream_t stream, aa_stream_t aux_stream);
 
 /* aa_greedy_decode with the T-step loop split over up to AA_MAX_LANES streams ("lanes"): the
  * encoder tail runs on `stream` for the whole batch, then lane i decodes its contiguous block of
@@ -205,7 +224,9 @@ AA_API int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t
  * captured once into a hipGraph (one graph launch replaces the ~4T+6 kernel launches; lanes, if
  * n_lanes > 1, are streams owned by the plan).  Launch it as often as needed on any stream; the
  * buffers it was created with are read/written at every launch.  Results equal aa_greedy_decode's
- * bit for bit.  The plan holds no device memory of its own besides the instantiated graph. */
+ * bit for bit.  With n_lanes <= 1 the plan captures aa_greedy_decode_aux's two-stream form (split
+ * LSTM steps) unless flags & AA_DECODE_FUSED_LSTM.  The plan holds no device memory of its own
+ * besides the instantiated graph. */
 typedef struct aa_decode_plan aa_decode_plan;
 AA_API int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int32_t T,
                                  int64_t* ids, float* alpha, float* beta, void* workspace,

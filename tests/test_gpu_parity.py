@@ -184,6 +184,25 @@ def test_graph_plan_replay_equals_direct(model, gpu_device, lanes, exact):
     assert not torch.equal(ref[0], ref2[0])
 
 
+@pytest.mark.parametrize("B,exact,graph", [(512, False, False), (77, False, False), (130, True, False),
+                                           (512, False, True), (77, False, True)])
+def test_split_lstm_step_equals_fused(model, gpu_device, B, exact, graph):
+    """The split LSTM step (k_lstm_gemm of step t+1 on the side stream beside step t's attention and
+    vocab stages, then k_lstm_cell) gives the one-launch k_lstm's results bit for bit, direct and
+    captured (graph: first call direct, second capture + launch, third replay)."""
+    feats = torch.from_numpy(synth.make_features(B, seed=31)).to(gpu_device)
+    ref = model.sampler(feats, max_len=11, exact_vocab=exact, graph=False)
+    model.split_lstm = True
+    try:
+        for _ in range(3 if graph else 1):
+            got = model.sampler(feats, max_len=11, exact_vocab=exact, graph=graph)
+            torch.cuda.synchronize()
+            for r, g in zip(ref, got):
+                assert torch.equal(r, g)
+    finally:
+        model.split_lstm = False
+
+
 def test_greedy_matches_oracle_odd_batch(model, oracle, gpu_device):
     B = 37
     feats = synth.make_features(B, seed=21)
