@@ -19,6 +19,7 @@ ABI_VERSION = 8
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
+DECODE_SCREEN64 = 8
 MAX_LANES = 8
 MAX_BEAM = 8
 

@@ -220,6 +220,8 @@ class Encoder2Decoder(nn.Module):
         # one-launch k_lstm at B = 512 (cross-stream hand-offs cost more than the overlap gains;
         # DESIGN.md §4), so off by default
         self.split_lstm = False
+        # True: vocab screen on 64 x 64 tiles (k_vscreen) instead of 128 x 160 (k_vscreen2); same ids
+        self.screen64 = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -419,7 +421,7 @@ class Encoder2Decoder(nn.Module):
         return cache[key]
 
     def _lstm_flags(self) -> int:
-        return 0 if self.split_lstm else _lib.DECODE_FUSED_LSTM
+        return (0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
 
     def _lanes(self, n: int, dev) -> list:
         """n side streams on ``dev`` (created once, reused)."""

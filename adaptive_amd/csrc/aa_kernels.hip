@@ -1305,6 +1305,127 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const 
   }
 }
 
+// Screen, wide-tile form (k_vscreen2): one 256-thread workgroup per 128 rows x 160 columns (5
+// granules), so at B = 512, V = 10,123 the grid is exactly 256 workgroups (4 row tiles x 64 column
+// tiles) and each CU moves 128 + 160 rows x H bf16 = 288 KB from L2 instead of the 64 x 64 form's
+// 5 x 128 KB: the 64 x 64 form is bound by those bytes per CU, not by the MFMAs.
+//   wave w owns the tile's rows 32w .. 32w+31 and all 5 column blocks (5 accumulators, K not split):
+//   its u fragments (its own 32 rows, all of K) go straight to VGPRs in one round trip; the W_m
+//   fragments of the 5 column blocks are shared by the 4 waves through LDS, staged in SC2_KS-chunk
+//   stages (register prefetch of stage s+1 under the MFMAs of stage s, two LDS buffers, one
+//   barrier per stage).  The epilogue is the 64 x 64 form's, per 32 x 32 block.
+constexpr int SC2_BM = 128, SC2_NB = 5, SC2_BN = 32 * SC2_NB, SC2_KS = 8;
+constexpr int SC2_STAGE = SC2_NB * SC2_KS * 64;  // bf16x8 per LDS stage (40 KB)
+
+// Per (row, granule) summary of one 32 x 32 block of screened logits in MFMA C layout (rows row0..,
+// columns 32 G..): keys, transposing top-2 butterfly, bound E, one float4 per row (see k_vscreen).
+__device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0, int G, float bv, float2 gsv,
+                                                  const float* __restrict__ un_blk, bool valid, int B, int NTn,
+                                                  float4* __restrict__ summ) {
+  const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  uint32_t k1[16], k2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t key = order_key(blk[r] + bv);
+    k1[r] = valid ? (key & ~31u) | (uint32_t)li : 0u;
+    k2[r] = 0u;
+  }
+  screen_bfly<16>(k1, k2, li);
+  screen_bfly<8>(k1, k2, li);
+  screen_bfly<4>(k1, k2, li);
+  screen_bfly<2>(k1, k2, li);
+  const uint32_t r1 = partner<1>(k1[0]), r2 = partner<1>(k2[0]);
+  const uint32_t m1 = k1[0] > r1 ? k1[0] : r1;
+  const uint32_t lo = k1[0] > r1 ? r1 : k1[0], h2 = k2[0] > r2 ? k2[0] : r2;
+  const uint32_t m2 = lo > h2 ? lo : h2;
+  const int rr = (li >> 1) & 15;  // this lane pair now holds row acc_row(rr) of the block
+  const int rl = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+  const int row = row0 + rl;
+  if (!(li & 1) && row < B) {
+    float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    if (m1) {
+      const float uw = un_blk[rl] * gsv.x;
+      const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+      const float x1 = key_value(m1 & ~31u);
+      const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
+      o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float(G * VS_TILE + (int)(m1 & 31u)));
+    }
+    summ[(int64_t)row * NTn + G] = o;
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                  float4* __restrict__ summ) {
+  constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
+  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
+  __shared__ float un_s[SC2_BM];
+  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NT);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31;
+  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  // this wave's u fragments: row block (m0 / 32 + wave), every k16 chunk -- one round trip
+  bf16x8 fa[KC];
+  {
+    const bf16x8* a0 = ua + (size_t)((m0 >> 5) + wave) * KC * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) fa[c] = a0[(size_t)c * 64];
+  }
+  // W stage s: for column block b (0..4), chunks [s KS, (s+1) KS) are one contiguous 8 KB run of the
+  // fragment-order W_m; thread t moves bf16x8 j = t + 256 i of the stage (b = j / (KS*64)).
+  const bf16x8* wbase = wf + (size_t)(n0 >> 5) * KC * 64;
+  bf16x8 wr[PER];
+  auto gload = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = t + 256 * i, b = j / (SC2_KS * 64), r = j - b * (SC2_KS * 64);
+      wr[i] = wbase[((size_t)b * KC + s * SC2_KS) * 64 + r];
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) Ws[buf][t + 256 * i] = wr[i];
+  };
+  // epilogue operands, loaded behind the fragments
+  if (t < SC2_BM) {
+    const int r = m0 + t;
+    un_s[t] = unorm[r < B ? r : B - 1];
+  }
+  const float bv0 = bias[n0 + li], bv1 = bias[n0 + 32 + li], bv2 = bias[n0 + 64 + li], bv3 = bias[n0 + 96 + li],
+              bv4 = bias[n0 + 128 + li];
+  floatx16 acc[SC2_NB];
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  gload(0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    lstore(s & 1);
+    if (s + 1 < NS) gload(s + 1);
+    __syncthreads();
+    const bf16x8* ws = Ws[s & 1] + lane;
+#pragma unroll
+    for (int c = 0; c < SC2_KS; ++c) {
+#pragma unroll
+      for (int b = 0; b < SC2_NB; ++b) {
+        const bf16x8 w = ws[(b * SC2_KS + c) * 64];
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s * SC2_KS + c], w, acc[b], 0, 0, 0);
+      }
+    }
+  }
+  const float bvs[SC2_NB] = {bv0, bv1, bv2, bv3, bv4};
+  const int row0 = m0 + 32 * wave;
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b) {
+    const int G = n0 / VS_TILE + b;
+    screen_block_summ(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
+  }
+}
+
 // Exact fp32 logit of one column, computed by a group of 8 lanes (lane8 = 0..7): lane8 j runs the
 // fma chain of partial j (K-steps [j*per, (j+1)*per) of 32, in the MFMA k order: pairs (s, 16+s)),
 // then the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) over xor-1/2/4 shuffles, then + bias.
@@ -1799,7 +1920,7 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.unorm = c.take<float>((size_t)B);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
   w.gates = c.take<float>((size_t)B * 4 * L.H);  // split LSTM step: h W_hh^T of the next step
-  w.ub = c.take<uint16_t>((size_t)((B + 63) / 64) * 64 * L.H);  // fragment order, 64-row tiles
+  w.ub = c.take<uint16_t>((size_t)((B + 127) / 128) * 128 * L.H);  // fragment order, 128-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
@@ -1962,9 +2083,10 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
 // sg != nullptr: split LSTM steps -- k_lstm_gemm for step t+1 (it needs only h_t) runs on sg beside
 // step t's attention, vocab screen and rescoring on s, and k_lstm_cell of step t+1 waits for it
 // (sg == s: the same kernels in stream order).  sg == nullptr: the fused k_lstm.
-static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, bool exact,
+static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, int32_t flags,
                        int64_t* ids, float* alpha, float* beta, const aa_trace* trace, hipStream_t s,
                        hipStream_t sg = nullptr) {
+  const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   const int H = L.H, MT = (Bl + 63) / 64, NTn = L.Vp / VS_TILE;
   const float* V = w.V + (size_t)r0 * P * H;
   const float* vwv = w.vwv + (size_t)r0 * P * PP;
@@ -2043,13 +2165,21 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   hipLaunchKernelGGL(k_vscreen<H_>, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.V, \
                      L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                        \
                      reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
+#define AA_SCREEN2(H_)                                                                                      \
+  hipLaunchKernelGGL(k_vscreen2<H_>, dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl, \
+                     L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
+                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
+      // wide tiles when the padded vocabulary is whole 160-column tiles (V = 10,123: 64 of them) and
+      // a wave's u fragments fit its registers
+      const bool wide = L.Vp % SC2_BN == 0 && H <= 512 && !(flags & AA_DECODE_SCREEN64);
       switch (H) {
-        case 256: AA_SCREEN(256); break;
-        case 512: AA_SCREEN(512); break;
+        case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
+        case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
         case 768: AA_SCREEN(768); break;
         default: AA_SCREEN(1024); break;
       }
 #undef AA_SCREEN
+#undef AA_SCREEN2
       rec(sev, 2 * t + 1, s);
       rec(rev, 2 * t, s);
       hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,
@@ -2102,7 +2232,7 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
     }
     // the split LSTM step uses the aux stream (if any) for the GEMM of the next step
     hipStream_t sg = (flags & AA_DECODE_FUSED_LSTM) || !aux || aux == ls ? nullptr : aux;
-    rc = decode_rows(L, p, w, B, 0, B, T, exact, ids, alpha, beta, trace, ls, sg);
+    rc = decode_rows(L, p, w, B, 0, B, T, flags, ids, alpha, beta, trace, ls, sg);
     if (rc) return rc;
     if (ls != s) {
       AA_TRY(hipEventRecord(e, ls));
@@ -2120,7 +2250,7 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
       if (r1 > B) r1 = B;
       hipStream_t ls = (hipStream_t)lanes[i];
       AA_TRY(hipStreamWaitEvent(ls, fork, 0));
-      rc = decode_rows(L, p, w, B, r0, r1 - r0, T, exact, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
+      rc = decode_rows(L, p, w, B, r0, r1 - r0, T, flags, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
       if (rc) return rc;
       AA_TRY(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
       AA_TRY(hipEventRecord(join[i], ls));

@@ -144,6 +144,8 @@ def main():
                     "finishes); 1 = one sampler() call after another")
     ap.add_argument("--split-lstm", action="store_true", help="split LSTM steps: k_lstm_gemm on a side stream "
                     "+ k_lstm_cell instead of the one-launch k_lstm (same results; slower at B=512)")
+    ap.add_argument("--screen64", action="store_true", help="vocab screen on 64x64 tiles (k_vscreen) instead of "
+                    "128x160 (k_vscreen2)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -161,6 +163,7 @@ def main():
     B, T = args.batch, args.max_len
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
     model.split_lstm = args.split_lstm
+    model.screen64 = args.screen64
     feats = synthetic_features(B, dev, seed=0, row0=rank * B)  # rows [rank*B, (rank+1)*B) of the global batch
     ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
 

@@ -177,6 +177,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 /* Decode flags */
 #define AA_DECODE_EXACT_VOCAB 1 /* compute every fp32 logit (fp32 MFMA GEMM + fused argmax) instead of
                                    the bf16 screen + exact fp32 rescoring; both give the same ids */
+#define AA_DECODE_SCREEN64 8 /* vocab screen on 64 x 64 tiles (k_vscreen) instead of the 128 x 160 tiles of
+                                k_vscreen2 (same summaries up to fp32 summation order; same ids) */
 #define AA_DECODE_FUSED_LSTM 4 /* aa_greedy_decode_aux / decode plans: keep the one-launch LSTM step
                                   (k_lstm) instead of the split k_lstm_gemm + k_lstm_cell */
 #define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of

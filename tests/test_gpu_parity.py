@@ -203,6 +203,22 @@ def test_split_lstm_step_equals_fused(model, gpu_device, B, exact, graph):
         model.split_lstm = False
 
 
+@pytest.mark.parametrize("B", [512, 300, 77, 4])
+def test_wide_screen_equals_screen64(model, gpu_device, B):
+    """The 128 x 160-tile screen (k_vscreen2) and the 64 x 64-tile one (k_vscreen) bound the same
+    logits: the decode's ids / alpha / beta are identical (the exact rescoring decides the ids)."""
+    feats = torch.from_numpy(synth.make_features(B, seed=41)).to(gpu_device)
+    got = model.sampler(feats, max_len=12, graph=False)
+    model.screen64 = True
+    try:
+        ref = model.sampler(feats, max_len=12, graph=False)
+    finally:
+        model.screen64 = False
+    torch.cuda.synchronize()
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+
+
 def test_greedy_matches_oracle_odd_batch(model, oracle, gpu_device):
     B = 37
     feats = synth.make_features(B, seed=21)
