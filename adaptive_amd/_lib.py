@@ -15,11 +15,12 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
 DECODE_SCREEN64 = 8
+DECODE_ENC_V3 = 16
 MAX_LANES = 8
 MAX_BEAM = 8
 

@@ -222,6 +222,9 @@ class Encoder2Decoder(nn.Module):
         self.split_lstm = False
         # True: vocab screen on 64 x 64 tiles (k_vscreen) instead of 128 x 160 (k_vscreen2); same ids
         self.screen64 = False
+        # True: encoder V GEMM on k_enc_v3 (128 x 128 tiles) instead of k_enc_v4 (two images per
+        # workgroup, all columns: the feature map is read once); same accuracy class
+        self.enc_v3 = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -421,7 +424,8 @@ class Encoder2Decoder(nn.Module):
         return cache[key]
 
     def _lstm_flags(self) -> int:
-        return (0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
+        return ((0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
+                | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0))
 
     def _lanes(self, n: int, dev) -> list:
         """n side streams on ``dev`` (created once, reused)."""
@@ -457,7 +461,8 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             rc = lib.aa_encoder_tail(model, images.data_ptr(), B, a_g.data_ptr(), V.data_ptr(), v_g.data_ptr(),
                                      h0.data_ptr(), c0.data_ptr(), VWv.data_ptr(),
-                                     _lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0, _lib.stream_handle())
+                                     (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
+                                     | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0), _lib.stream_handle())
         _lib.check(rc, "encoder_tail")
         return V, v_g, (h0, c0), a_g, VWv
 

@@ -61,7 +61,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3;
+  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3, enc_w4;
   size_t total_floats;
 };
 
@@ -98,12 +98,13 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_gs = take((size_t)2 * (L.Vp / VS_TILE));  // float2 per granule: (max ||w_n||, max |b_n|)
   L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
   L.mlp_w3 = take((size_t)3 * L.Vp * L.H / 2);    // W_m as 3 bf16 planes, fragments [Vp/32][H/16][3][64][8] (beam)
+  L.enc_w4 = take((size_t)3 * L.H * L.C / 2);     // W_a as 3 bf16 planes, 16x16x32 fragments [H/16][C/32][3][64][8]
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const bf16x8 *enc_w3, *whh3, *mlp_w3;
+  const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const float2* mlp_gs;
@@ -117,6 +118,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.enc_w3 = reinterpret_cast<const bf16x8*>(b + L.enc_w3);
   p.whh3 = reinterpret_cast<const bf16x8*>(b + L.whh3);
   p.mlp_w3 = reinterpret_cast<const bf16x8*>(b + L.mlp_w3);
+  p.enc_w4 = reinterpret_cast<const bf16x8*>(b + L.enc_w4);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -387,6 +389,161 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
       const int row = mt * EV_BM + a * 32 + acc_row(i, lane);
       if (row < M) V[(int64_t)row * H + col] = reluf_(acc[a][i] + bv);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// E1 (default at H = 128 NCB): the same bf16x3 V, one workgroup per TWO IMAGES and all H columns,
+// so the feature map is read from HBM exactly once and the grid is B/2 workgroups (256 at
+// B = 512: one per CU).  k_enc_v3's 128 x 128 tiles re-read every A row block once per column
+// tile (4x the A traffic through L2, 431 MB of HBM per launch against 260 MB algorithmic).
+//   rows: the 98 rows m = 98 wg .. 98 wg + 97 (images 2 wg, 2 wg + 1), computed as 7 blocks of
+//         16 rows of v_mfma_f32_16x16x32_bf16 (rows 98..111 of the tile are never stored);
+//   columns: wave w owns NCB 16-column blocks [16 NCB w, 16 NCB (w + 1)), all 7 row blocks
+//         (7 NCB accumulators of 4 floats);
+//   A: 16 dword loads per thread per 32-channel stage (lanes over consecutive rows: contiguous
+//      addresses), split in registers, three bf16 planes [row][k] in LDS with a 96-B pitch
+//      (conflict-free 16x16x32 ds_read_b128 fragment reads), double-buffered, one stage ahead;
+//   W: pre-split at pack time in 16x16x32 B-fragment order (enc_w4[nb][kc][q][lane][8], lane l
+//      holds W[16 nb + (l & 15)][32 kc + 8 (l >> 4) + j]); each column pair's fragments of stage
+//      s + 1 are loaded straight into VGPRs right after the pair's last MFMA of stage s.
+// The six products per block run smallest first, as in k_enc_v3 (fp32-accurate).
+// The avg-pool a_g (k_avgpool) is fused: the staging threads also put each stage's fp32 values in
+// LDS as [image][channel][p], and one wave per stage (rotating) sums every channel of both images
+// sequentially in p order and divides by 49 -- k_avgpool's arithmetic, bit-identical to ATen.
+// ---------------------------------------------------------------------------------------------
+constexpr int E4_ROWS = 98, E4_RB = 7, E4_LD = 48;  // rows per workgroup, 16-row blocks, LDS pitch (bf16)
+constexpr int E4_SP = 52, E4_MAXC = 2048;           // a_g staging pitch (floats), largest channel count
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int NCB>
+__global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats, int B, int C,
+                                                const bf16x8* __restrict__ W4, const float* __restrict__ bias,
+                                                float* __restrict__ V, float* __restrict__ a_g) {
+  static_assert(NCB % 2 == 0, "columns are processed in pairs of 16-column blocks");
+  constexpr int H = 128 * NCB, NPAIR = NCB / 2, PL = E4_RB * 16 * E4_LD;  // PL: one plane, bf16
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][PL];
+  __shared__ __attribute__((aligned(16))) float Sg[2][2 * 32 * E4_SP];  // fp32 stage copy for a_g
+  __shared__ __attribute__((aligned(16))) float Ag[2 * E4_MAXC];        // a_g of the two images
+  const int M = B * P, KC = C / 32;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = blockIdx.x * E4_ROWS;
+  // staging: thread t < 392 -> row r = t % 98, channels 8 kg .. 8 kg + 7 of each 32-channel stage;
+  // threads 392..511 fill garbage rows 98..105 (never stored) from a valid address
+  const int sr = t < 4 * E4_ROWS ? t % E4_ROWS : E4_ROWS + (t & 7);
+  const int kg = t < 4 * E4_ROWS ? t / E4_ROWS : (t >> 3) & 3;
+  int m = m0 + (t < 4 * E4_ROWS ? sr : 0);
+  m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
+  const int bi = m / P, pi = m - bi * P;
+  const float* arow = feats + (int64_t)bi * C * P + pi + (int64_t)(8 * kg) * P;
+  const int so = sr * E4_LD + 8 * kg;
+  // fragment reads: lane l -> row 16 rb + (l & 15), k = 8 (l >> 4)
+  const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);
+  const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;  // block nb = wave NCB + c
+  float ra[8];
+  bf16x8 wv[NCB][3];
+  floatx4 acc[E4_RB][NCB];
+#pragma unroll
+  for (int rb = 0; rb < E4_RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto gload_a = [&](int s) {
+    const float* src = arow + (int64_t)(32 * s) * P;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = src[i * P];
+  };
+  auto gload_w = [&](int s, int c) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)s * 3 + q) * 64];
+  };
+  auto lstore_a = [&](int buf) {
+    bf16x8 x[3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __bf16 x0, x1, x2;
+      split3(ra[i], x0, x1, x2);
+      x[0][i] = x0; x[1][i] = x1; x[2][i] = x2;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&As[buf][q][so]) = x[q];
+    if (t < 4 * E4_ROWS) {  // sr = 49 image + p
+      const int img = sr >= P, pp = sr - img * P;
+      float* g = &Sg[buf][(img * 32 + 8 * kg) * E4_SP + pp];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i * E4_SP] = ra[i];
+    }
+  };
+
+  const int ns = KC;
+  gload_a(0);
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) gload_w(0, c);
+  lstore_a(0);
+  gload_a(ns > 1 ? 1 : 0);
+  __syncthreads();
+  for (int s = 0; s < ns; ++s) {
+    const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
+    // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
+    lstore_a(buf ^ 1);
+    gload_a(s2);
+    __builtin_amdgcn_sched_barrier(0);
+    const __bf16* Ab = &As[buf][0][fo];
+#pragma unroll
+    for (int cp = 0; cp < NPAIR; ++cp) {
+#pragma unroll
+      for (int rb = 0; rb < E4_RB; ++rb) {
+        bf16x8 fa[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(Ab + q * PL + rb * 16 * E4_LD);
+#pragma unroll
+        for (int c = 2 * cp; c < 2 * cp + 2; ++c) {
+          floatx4 x = acc[rb][c];
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][2], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][0], x, 0, 0, 0);
+          acc[rb][c] = x;
+        }
+      }
+      gload_w(s1, 2 * cp);
+      gload_w(s1, 2 * cp + 1);
+      // re-read the A fragments for the next pair instead of keeping all 21 live (VGPR budget)
+      asm volatile("" ::: "memory");
+    }
+    if (wave == (s & 7)) {  // a_g of stage s's 32 channels: lane -> (image lane / 32, channel lane % 32)
+      const float* g = &Sg[buf][lane * E4_SP];
+      float sum = 0.f;
+#pragma unroll 4
+      for (int pp = 0; pp < 48; pp += 4) {  // 16-B reads (E4_SP * 4 B = 13 x 16 B), summed in p order
+        const float4 v = *reinterpret_cast<const float4*>(g + pp);
+        sum += v.x; sum += v.y; sum += v.z; sum += v.w;
+      }
+      sum += g[48];
+      Ag[(lane >> 5) * C + 32 * s + (lane & 31)] = sum / 49.0f;
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // a_g of the workgroup's images (the last workgroup of an odd batch holds one)
+  for (int i = t; i < 2 * C; i += 512) {
+    const int img = 2 * blockIdx.x + (i >= C);
+    if (img < B) a_g[(int64_t)img * C + (i - (i >= C ? C : 0))] = Ag[i];
+  }
+  // epilogue: lane l holds column 16 nb + (l & 15), rows 16 rb + 4 (l >> 4) + i
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int col = (wave * NCB + c) * 16 + (lane & 15);
+    const float bv = bias[col];
+#pragma unroll
+    for (int rb = 0; rb < E4_RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rb * 16 + 4 * (lane >> 4) + i, row = m0 + r;
+        if (r < E4_ROWS && row < M) V[(int64_t)row * H + col] = reluf_(acc[rb][c][i] + bv);
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1642,6 +1799,24 @@ __global__ void k_pack_w3(const float* __restrict__ w, int C, bf16x8* __restrict
   o[128] = lo;
 }
 
+// W_a split into three bf16 planes in 16x16x32 B-fragment order (see k_enc_v4): block = (nb, kc),
+// lane l -> W[16 nb + (l & 15)][32 kc + 8 (l >> 4) + j], planes at out[((nb KC + kc) 3 + q) 64 + l].
+__global__ void k_pack_w4(const float* __restrict__ w, int C, bf16x8* __restrict__ out) {
+  const int KC = C / 32, nb = blockIdx.x / KC, kc = blockIdx.x % KC, l = threadIdx.x;
+  const float* src = w + (int64_t)(16 * nb + (l & 15)) * C + 32 * kc + 8 * (l >> 4);
+  bf16x8 h, m, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 a, b, c;
+    split3(src[j], a, b, c);
+    h[j] = a; m[j] = b; lo[j] = c;
+  }
+  bf16x8* o = out + ((size_t)blockIdx.x * 3) * 64 + l;
+  o[0] = h;
+  o[64] = m;
+  o[128] = lo;
+}
+
 __global__ void k_pack_wgs(const float* __restrict__ wg, const float* __restrict__ ws, int H, float* __restrict__ out) {
   const int tile = blockIdx.x;
   for (int i = threadIdx.x; i < 2 * P * 16; i += blockDim.x) {
@@ -1788,6 +1963,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                      reinterpret_cast<bf16x8*>(base + L.whh3));
   hipLaunchKernelGGL(k_pack_w3, dim3((L.Vp / 32) * (H / 16)), dim3(64), 0, s, base + L.mlp_w, H,
                      reinterpret_cast<bf16x8*>(base + L.mlp_w3));
+  hipLaunchKernelGGL(k_pack_w4, dim3((H / 16) * (C / 32)), dim3(64), 0, s, w->enc_affine_a_w, C,
+                     reinterpret_cast<bf16x8*>(base + L.enc_w4));
   return launch_status();
 }
 
@@ -1812,28 +1989,52 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     AA_TRY(hipStreamWaitEvent(aux, fork, 0));
     sa = aux;
   }
-  rec(ev, 0, sa);
-  hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, sa, feats, nch, a_g);
-  rec(ev, 1, sa);
-  rec(ev, 4, sa);
-  {
+  auto heads_xg = [&](hipStream_t st) {
+    rec(ev, 4, st);
     const int MT = (B + 63) / 64, NTn = L.NHp / 64;
-    hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, sa, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
+    hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
                        v_g, h0, c0);
-  }
-  rec(ev, 5, sa);
-  rec(ev, 8, sa);
-  if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, sa);
-  rec(ev, 9, sa);
-  rec(ev, 2, s);
-  if (flags & AA_DECODE_FP32_ENCODER) {
-    const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
-    hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
+    rec(ev, 5, st);
+    rec(ev, 8, st);
+    if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
+    rec(ev, 9, st);
+  };
+  const bool v4 = !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && (H == 512 || H == 256) && C <= E4_MAXC;
+  if (v4) {
+    // k_enc_v4 computes V and a_g in one pass over the feature map; the a_g branch (heads, x_g)
+    // then runs on aux beside the VWv GEMM.  (Trace: the fused avg-pool is a zero-length pair.)
+    rec(ev, 0, s);
+    rec(ev, 1, s);
+    rec(ev, 2, s);
+    const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
+    if (H == 512)
+      hipLaunchKernelGGL(k_enc_v4<4>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+    else
+      hipLaunchKernelGGL(k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+    rec(ev, 3, s);
+    if (sa != s) {  // aux waits for a_g
+      hipEvent_t agr = nullptr;
+      AA_TRY(hipEventCreateWithFlags(&agr, hipEventDisableTiming));
+      AA_TRY(hipEventRecord(agr, s));
+      AA_TRY(hipStreamWaitEvent(sa, agr, 0));
+      AA_TRY(hipEventDestroy(agr));
+    }
+    heads_xg(sa);
   } else {
-    const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN;
-    hipLaunchKernelGGL(k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_w3, p.enc_a_b, V);
+    rec(ev, 0, sa);
+    hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, sa, feats, nch, a_g);
+    rec(ev, 1, sa);
+    heads_xg(sa);
+    rec(ev, 2, s);
+    if (flags & AA_DECODE_FP32_ENCODER) {
+      const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
+      hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
+    } else {
+      const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN;
+      hipLaunchKernelGGL(k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_w3, p.enc_a_b, V);
+    }
+    rec(ev, 3, s);
   }
-  rec(ev, 3, s);
   rec(ev, 6, s);
   if (VWv) gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
   rec(ev, 7, s);

@@ -71,6 +71,7 @@ def kernel_costs(B: int, T: int) -> dict:
     f = flops_per_caption(T)
     return {
         "k_avgpool": ("hbm", B * C * (P + 1) * 4),                       # read A once, write a_g
+        "k_enc_v4": ("mfma_x3", f["k_enc_v"] * B),  # + the fused avg-pool (not priced)
         "k_enc_v3": ("mfma_x3", f["k_enc_v"] * B),
         "k_enc_heads": ("mfma", f["k_enc_heads"] * B),
         "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),
@@ -146,6 +147,8 @@ def main():
                     "+ k_lstm_cell instead of the one-launch k_lstm (same results; slower at B=512)")
     ap.add_argument("--screen64", action="store_true", help="vocab screen on 64x64 tiles (k_vscreen) instead of "
                     "128x160 (k_vscreen2)")
+    ap.add_argument("--enc-v3", action="store_true", help="encoder V GEMM on k_enc_v3 (128x128 tiles) instead of "
+                    "k_enc_v4 (two images per workgroup, all columns)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -164,6 +167,8 @@ def main():
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
     model.split_lstm = args.split_lstm
     model.screen64 = args.screen64
+    model.enc_v3 = args.enc_v3
+    enc_name = "k_enc_v3" if args.enc_v3 else "k_enc_v4"
     feats = synthetic_features(B, dev, seed=0, row0=rank * B)  # rows [rank*B, (rank+1)*B) of the global batch
     ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
 
@@ -232,14 +237,17 @@ def main():
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
         lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
-        per = {k: [] for k in ("k_avgpool", "k_enc_v3", "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)",
-                               lstm, "k_atten", "k_vscreen", "k_vrescore")}
+        enc_names = ("k_avgpool", enc_name, "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)")
+        per = {k: [] for k in enc_names + (lstm, "k_atten", "k_vscreen", "k_vrescore")}
+        if not args.enc_v3:
+            del per["k_avgpool"]  # fused into k_enc_v4 (its trace pair is empty)
         if model.split_lstm:
             per["k_lstm_gemm"] = []
         for ev, _ in traces:
             enc = ev["encoder"].pair_durations_ms()
-            for i, k in enumerate(("k_avgpool", "k_enc_v3", "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)")):
-                per[k].append(enc[i])
+            for i, k in enumerate(enc_names):
+                if k in per:
+                    per[k].append(enc[i])
             per[lstm] += ev["lstm"].pair_durations_ms()
             if model.split_lstm:
                 per["k_lstm_gemm"] += ev["gemm"].pair_durations_ms()

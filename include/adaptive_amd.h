@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 8
+#define AA_ABI_VERSION 9
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -182,7 +182,9 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 #define AA_DECODE_FUSED_LSTM 4 /* aa_greedy_decode_aux / decode plans: keep the one-launch LSTM step
                                   (k_lstm) instead of the split k_lstm_gemm + k_lstm_cell */
 #define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of
-                                    the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v3) */
+                                    the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v4) */
+#define AA_DECODE_ENC_V3 16 /* V on the 128 x 128-tile bf16x3 kernel (k_enc_v3) instead of k_enc_v4 (one
+                               workgroup per two images, all H columns; H in {256, 512}) */
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];
