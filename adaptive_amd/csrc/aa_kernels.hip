@@ -61,7 +61,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3, enc_w4;
+  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3, enc_w4, heads_w4;
   size_t total_floats;
 };
 
@@ -99,12 +99,13 @@ static Layout make_layout(const aa_dims& d) {
   L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
   L.mlp_w3 = take((size_t)3 * L.Vp * L.H / 2);    // W_m as 3 bf16 planes, fragments [Vp/32][H/16][3][64][8] (beam)
   L.enc_w4 = take((size_t)3 * L.H * L.C / 2);     // W_a as 3 bf16 planes, 16x16x32 fragments [H/16][C/32][3][64][8]
+  L.heads_w4 = take((size_t)3 * L.NHp * L.C / 2);  // heads as 3 bf16 planes, 16x16x32 fragments [NHp/16][C/32][3][64][8]
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4;
+  const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4, *heads_w4;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const float2* mlp_gs;
@@ -119,6 +120,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.whh3 = reinterpret_cast<const bf16x8*>(b + L.whh3);
   p.mlp_w3 = reinterpret_cast<const bf16x8*>(b + L.mlp_w3);
   p.enc_w4 = reinterpret_cast<const bf16x8*>(b + L.enc_w4);
+  p.heads_w4 = reinterpret_cast<const bf16x8*>(b + L.heads_w4);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -570,6 +572,104 @@ __global__ __launch_bounds__(256) void k_enc_heads(const float* __restrict__ a_g
     const int row = mt * BM + wm * 32 + acc_row(r, lane);
     if (row >= B) continue;
     const float x = acc[0][0][r] + bv;
+    if (col < E) v_g[(int64_t)row * E + col] = reluf_(x);
+    else if (col < E + H) h0[(int64_t)row * H + (col - E)] = tanhf(x);
+    else c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// E2 (default): the heads on bf16 MFMA with 3-way split operands (fp32-accurate, as k_enc_v4).
+// k_enc_heads' 64 x 64 fp32-MFMA tiles give 160 workgroups that each run all K = 2048 (≈66 µs);
+// here a workgroup owns 32 rows x 16 NB columns (grid (B/32) x (NHp / 16 NB): 256 workgroups at
+// B = 512, NB = 5), its four waves each run a quarter of K over the whole tile (v_mfma_f32_16x16x32
+// _bf16; a_g fragments split in registers, W pre-split in 16x16x32 B-fragment order, heads_w4), and
+// the four partial tiles are summed in LDS as ((p0 + p1) + (p2 + p3)) before bias and activation.
+// ---------------------------------------------------------------------------------------------
+template <int NB>
+__global__ __launch_bounds__(256) void k_enc_heads3(const float* __restrict__ a_g, int B, int C, int E, int H,
+                                                    const bf16x8* __restrict__ W4, const float* __restrict__ bias,
+                                                    float* __restrict__ v_g, float* __restrict__ h0,
+                                                    float* __restrict__ c0) {
+  constexpr int BN = 16 * NB, TP = BN + 4;  // tile columns, LDS row pitch of a partial tile (floats)
+  __shared__ __attribute__((aligned(16))) float Pt[4][32 * TP];
+  const int KC = C / 32, NTn = (E + 2 * H + BN - 1) / BN;
+  const int mt = blockIdx.x / NTn, nt = blockIdx.x % NTn;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = mt * 32;
+  const float* arow[2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    int m = m0 + 16 * rb + (lane & 15);
+    m = m < B ? m : B - 1;  // clamp, never zero (rows >= B are not stored)
+    arow[rb] = a_g + (int64_t)m * C + 8 * (lane >> 4);
+  }
+  const bf16x8* wsrc = W4 + (size_t)(nt * NB) * KC * 3 * 64 + lane;
+  floatx4 acc[2][NB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int c = 0; c < NB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int per = KC / 4, kc0 = wave * per;  // C % 256 == 0 (checked by the host): per is even
+  float4 av[2][2][2];   // [slot][row block][half]
+  bf16x8 wv[2][NB][3];  // [slot][column block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      av[slot][rb][0] = *reinterpret_cast<const float4*>(arow[rb] + 32 * kc);
+      av[slot][rb][1] = *reinterpret_cast<const float4*>(arow[rb] + 32 * kc + 4);
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) wv[slot][c][q] = wsrc[((size_t)c * KC * 3 + (size_t)kc * 3 + q) * 64];
+  };
+  auto step = [&](int slot) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __bf16 x0, x1, x2;
+        split3(f4c(av[slot][rb][i >> 2], i & 3), x0, x1, x2);
+        fa[0][i] = x0; fa[1][i] = x1; fa[2][i] = x2;
+      }
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        floatx4 x = acc[rb][c];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[slot][c][0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[slot][c][1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[slot][c][2], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[slot][c][0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[slot][c][1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[slot][c][0], x, 0, 0, 0);
+        acc[rb][c] = x;
+      }
+    }
+  };
+  // two chunks in flight; `per` is even; past the end the chunk index is clamped (harmless reloads)
+  const int last = kc0 + per - 1;
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  for (int kc = kc0; kc < kc0 + per; kc += 2) {
+    step(0);
+    load(0, kc + 2 < last ? kc + 2 : last);
+    step(1);
+    load(1, kc + 3 < last ? kc + 3 : last);
+  }
+  // partial tile of this wave -> LDS [row][col]: lane holds column 16 c + (l & 15), rows 16 rb + 4 (l >> 4) + i
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Pt[wave][(16 * rb + 4 * (lane >> 4) + i) * TP + 16 * c + (lane & 15)] = acc[rb][c][i];
+  __syncthreads();
+  for (int e = t; e < 32 * BN; e += 256) {
+    const int r = e / BN, cl = e - r * BN, row = m0 + r, col = nt * BN + cl;
+    if (row >= B || col >= E + 2 * H) continue;
+    const int o = r * TP + cl;
+    const float x = ((Pt[0][o] + Pt[1][o]) + (Pt[2][o] + Pt[3][o])) + bias[col];
     if (col < E) v_g[(int64_t)row * E + col] = reluf_(x);
     else if (col < E + H) h0[(int64_t)row * H + (col - E)] = tanhf(x);
     else c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
@@ -1965,6 +2065,8 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                      reinterpret_cast<bf16x8*>(base + L.mlp_w3));
   hipLaunchKernelGGL(k_pack_w4, dim3((H / 16) * (C / 32)), dim3(64), 0, s, w->enc_affine_a_w, C,
                      reinterpret_cast<bf16x8*>(base + L.enc_w4));
+  hipLaunchKernelGGL(k_pack_w4, dim3((L.NHp / 16) * (C / 32)), dim3(64), 0, s, base + L.heads_w, C,
+                     reinterpret_cast<bf16x8*>(base + L.heads_w4));
   return launch_status();
 }
 
@@ -1991,9 +2093,18 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
   }
   auto heads_xg = [&](hipStream_t st) {
     rec(ev, 4, st);
-    const int MT = (B + 63) / 64, NTn = L.NHp / 64;
-    hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
-                       v_g, h0, c0);
+    const int NH = E + 2 * H;
+    if (flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER) || C % 256) {
+      const int MT = (B + 63) / 64, NTn = L.NHp / 64;
+      hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
+                         v_g, h0, c0);
+    } else if (NH % 80 == 0) {
+      hipLaunchKernelGGL(k_enc_heads3<5>, dim3(((B + 31) / 32) * (NH / 80)), dim3(256), 0, st, a_g, B, C, E, H,
+                         p.heads_w4, p.heads_b, v_g, h0, c0);
+    } else {
+      hipLaunchKernelGGL(k_enc_heads3<4>, dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st, a_g, B, C, E,
+                         H, p.heads_w4, p.heads_b, v_g, h0, c0);
+    }
     rec(ev, 5, st);
     rec(ev, 8, st);
     if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);

@@ -74,6 +74,7 @@ def kernel_costs(B: int, T: int) -> dict:
         "k_enc_v4": ("mfma_x3", f["k_enc_v"] * B),  # + the fused avg-pool (not priced)
         "k_enc_v3": ("mfma_x3", f["k_enc_v"] * B),
         "k_enc_heads": ("mfma", f["k_enc_heads"] * B),
+        "k_enc_heads3": ("mfma_x3", f["k_enc_heads"] * B),
         "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),
         "k_gemm_bias(x_g)": ("mfma", f["xg"] * B),
         "k_lstm": ("mfma_x3", f["k_lstm"] * B),
@@ -237,7 +238,8 @@ def main():
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
         lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
-        enc_names = ("k_avgpool", enc_name, "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)")
+        enc_names = ("k_avgpool", enc_name, "k_enc_heads" if args.enc_v3 else "k_enc_heads3", "k_gemm_bias(VWv)",
+                     "k_gemm_bias(x_g)")
         per = {k: [] for k in enc_names + (lstm, "k_atten", "k_vscreen", "k_vrescore")}
         if not args.enc_v3:
             del per["k_avgpool"]  # fused into k_enc_v4 (its trace pair is empty)

@@ -73,10 +73,12 @@ def test_split_bf16_encoder_is_fp32_accurate(model, oracle, gpu_device, B):
     fp32 accumulation), far below the 2e-5 parity tolerance.  B = 67 -> 3283 rows: a ragged last
     128-row tile (v3) and a last two-image workgroup holding one image (v4); B = 512: the bench grid."""
     feats = torch.from_numpy(synth.make_features(B, seed=3)).to(gpu_device)
-    V4 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
+    out4 = model._encode(feats)
+    V4 = out4[0].cpu().numpy().astype(np.float64)
     try:
         model.enc_v3 = True
-        V3 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
+        out3 = model._encode(feats)
+        V3 = out3[0].cpu().numpy().astype(np.float64)
         model.enc_v3 = False
         model.fp32_encoder = True
         V1 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
@@ -95,6 +97,20 @@ def test_split_bf16_encoder_is_fp32_accurate(model, oracle, gpu_device, B):
         assert ex.max() < 2e-6, (name, ex.max())        # fp32 GEMM class: ~K u / sqrt(K) << 1e-5
         assert ex.max() < 4 * e1.max() + 1e-7, (name, ex.max(), e1.max())
         assert np.abs(Vx - ref).max() < ATT_TOL / 2, name
+    # heads: k_enc_heads3 (bf16x3, default) and k_enc_heads (fp32 MFMA, with k_enc_v3) vs fp64
+    a_g = out4[3].cpu().numpy().astype(np.float64)
+    assert np.array_equal(out4[3].cpu().numpy(), out3[3].cpu().numpy()), "fused avg-pool == k_avgpool"
+    for key, act, got4, got3 in (("encoder.affine_b", np.maximum, out4[1], out3[1]),
+                                 ("encoder.affine_h0", np.tanh, out4[2][0][:, 0], out3[2][0][:, 0]),
+                                 ("encoder.affine_c0", np.tanh, out4[2][1][:, 0], out3[2][1][:, 0])):
+        Wh = oracle.w[key + ".weight"].numpy().astype(np.float64)
+        bh = oracle.w[key + ".bias"].numpy().astype(np.float64)
+        pre = a_g @ Wh.T + bh
+        r = np.maximum(pre, 0.0) if act is np.maximum else np.tanh(pre)
+        sc = np.abs(a_g) @ np.abs(Wh).T + np.abs(bh)
+        e4 = np.abs(got4.cpu().numpy() - r) / sc
+        e3 = np.abs(got3.cpu().numpy() - r) / sc
+        assert e4.max() < 2e-6 and e4.max() < 4 * e3.max() + 1e-7, (key, e4.max(), e3.max())
 
 
 def test_decode_step_logits(model, oracle, gpu_device):
