@@ -222,6 +222,159 @@ __global__ __launch_bounds__(512) void kv_ls(int B, int V, const int64_t* __rest
     }
   }
 }
+template <int H, int MODE>
+__global__ __launch_bounds__(512) void kv_at(int B, int kdiv, const float* __restrict__ h_new,
+                                                const float* __restrict__ s_new, const float* __restrict__ part,
+                                                const float* __restrict__ Vf, const float* __restrict__ VWv,
+                                                const float* __restrict__ wh, float* __restrict__ alpha_out,
+                                                int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
+                                                float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
+                                                float* __restrict__ unorm, bf16x8* __restrict__ ub3_out) {
+  constexpr int DPT = H / 512, NT16 = H / 16, NG = NT16 / 4;
+  __shared__ float red[4][128];
+  __shared__ float proj[PART];
+  __shared__ float zs[PP];
+  __shared__ float sh_alpha[PP];
+  __shared__ float sh_beta;
+  __shared__ float sh_norm[8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = blockIdx.x;
+  const int img = kdiv == 1 ? b : b / kdiv;
+  // loads, oldest first in the order they are consumed; clamped addresses, no branches
+  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
+  float pv[NG];
+  {
+    const float* pp = part + ((int64_t)b * NT16 + grp) * PART + jpc;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) pv[i] = pp[(int64_t)4 * i * PART];
+  }
+  const int k = t >> 3, q = t & 7;
+  const int kc = k < P ? k : P - 1;
+  const float* vw = VWv + ((int64_t)img * P + kc) * PP;
+  float vwr[7], whr[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+    vwr[i] = vw[j];
+    whr[i] = q + 8 * i < P ? wh[j] : 0.f;
+  }
+  const float* vb = Vf + (int64_t)img * P * H;
+  float hv[DPT], sv[DPT];
+  if (MODE >= 2) {
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      hv[i] = h_new[(int64_t)b * H + t + 512 * i];
+      sv[i] = s_new[(int64_t)b * H + t + 512 * i];
+    }
+    if (MODE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  float vv[DPT][P];
+#pragma unroll
+  for (int i = 0; i < DPT; ++i)
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) vv[i][kk] = MODE == 1 ? (float)(kk + t) * 1e-3f : vb[(int64_t)kk * H + t + 512 * i];
+  if (MODE < 2) {
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    hv[i] = h_new[(int64_t)b * H + t + 512 * i];
+    sv[i] = s_new[(int64_t)b * H + t + 512 * i];
+  }
+  }
+  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
+  {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) a += pv[i];
+    red[grp][jp] = a;
+  }
+  __syncthreads();
+  if (t < 2 * P) proj[t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  __syncthreads();
+  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+      const float x = (k < P ? vwr[i] : proj[P + j]) + proj[j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
+    }
+    z = z + __shfl_xor(z, 1, 64);
+    z = z + __shfl_xor(z, 2, 64);
+    z = z + __shfl_xor(z, 4, 64);
+    if (q == 0 && k <= P) zs[k] = z;
+  }
+  __syncthreads();
+  // 3) softmax (wave 0)
+  if (w == 0) {
+    const float z = lane < P ? zs[lane] : -INFINITY;
+    const float zsn = zs[P];
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float S = wave_sum(e);
+    const float a = e / S;
+    if (lane < P) {
+      sh_alpha[lane] = a;
+      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
+    }
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      const float beta = es / S2;
+      sh_beta = beta;
+      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
+    }
+  }
+  __syncthreads();
+  // 4) context + u
+  const float beta = sh_beta;
+  float nsq = 0.f;
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int d = t + 512 * i;
+    float c = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sh_alpha[kk], vv[i][kk], c);
+    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
+    const float u = chat + hv[i];
+    nsq = __builtin_fmaf(u, u, nsq);
+    u_out[(int64_t)b * H + d] = u;
+    if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+    if (ub3_out) {
+      __bf16 x0, x1, x2;
+      split3(u, x0, x1, x2);
+      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+      o[0] = x0;
+      o[64 * 8] = x1;
+      o[128 * 8] = x2;
+    }
+  }
+  if (unorm) {
+    nsq = wave_sum(nsq);
+    if (lane == 0) sh_norm[w] = nsq;
+    __syncthreads();
+    if (t == 0)
+      unorm[b] = sqrtf(((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) +
+                       ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.00001f;
+  }
+}
+
+// MODE 0: V stream only (same loads as k_atten5), one float out per thread
+__global__ __launch_bounds__(512) void kv_vstream(const float* __restrict__ Vf, float* __restrict__ out) {
+  constexpr int H = 512;
+  const int t = threadIdx.x, b = blockIdx.x;
+  const float* vb = Vf + (int64_t)b * P * H;
+  float vv[P];
+#pragma unroll
+  for (int kk = 0; kk < P; ++kk) vv[kk] = vb[(int64_t)kk * H + t];
+  float c = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < P; ++kk) c += vv[kk];
+  out[(int64_t)b * H + t] = c;
+}
 // VARIANTS END
 }  // namespace aa
 
@@ -275,6 +428,27 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
       auto kern = kv_ls<3>;
       hipLaunchKernelGGL(kern, dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
                          p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "at_nov")) {
+      hipLaunchKernelGGL((kv_at<512, 1>), dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
+                         (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
+    } else if (!strcmp(which, "at_copy")) {
+      hipLaunchKernelGGL((kv_at<512, 0>), dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
+                         (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
+    } else if (!strcmp(which, "vstream")) {
+      hipLaunchKernelGGL(kv_vstream, dim3(B), dim3(512), 0, s, w.V, w.s);
+    } else if (!strcmp(which, "vscreen2")) {
+      hipLaunchKernelGGL(k_vscreen2<512>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, B,
+                         L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,
+                         reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ);
+    } else if (!strcmp(which, "enc_v4")) {
+      hipLaunchKernelGGL(k_enc_v4<4>, dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "at_wait")) {
+      hipLaunchKernelGGL((kv_at<512, 2>), dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
+                         (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
+    } else if (!strcmp(which, "at_hsfirst")) {
+      hipLaunchKernelGGL((kv_at<512, 3>), dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
+                         (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
     // VARIANT LAUNCH END
     } else {
       return false;
