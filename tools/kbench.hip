@@ -375,6 +375,259 @@ __global__ __launch_bounds__(512) void kv_vstream(const float* __restrict__ Vf, 
   for (int kk = 0; kk < P; ++kk) c += vv[kk];
   out[(int64_t)b * H + t] = c;
 }
+template <int H, int MODE>
+__device__ __forceinline__ void kv_tail(int B, int m0, int nt, const float (&gate)[4][2], float2 sa, float2 sb,
+                                               float2 cprev, float4 wsv, float* Hs, float* h_out,
+                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                               float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int HP = LS_HP, WSP = LS_WSP, NTn = H / 16, KC = H / 16;
+  float* Ss = Hs + 16 * HP;   // [16][HP] s of the tile, transposed
+  float* Wsl = Ss + 16 * HP;  // [16][WSP] W_g / W_s rows (j < 49: W_g, else W_s) per unit
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr, j = nt * 16 + u0;
+  {  // transpose the W_g / W_s slice to [unit][j] (j = 98, 99 are zero)
+    const int jj = t >> 2, uq = (t & 3) * 4;
+    if (t < 2 * P * 4) {
+      Wsl[(uq + 0) * WSP + jj] = wsv.x; Wsl[(uq + 1) * WSP + jj] = wsv.y;
+      Wsl[(uq + 2) * WSP + jj] = wsv.z; Wsl[(uq + 3) * WSP + jj] = wsv.w;
+    } else if (t < 2 * P * 4 + 32) {
+      const int z = t - 2 * P * 4;  // 32 zeros: j = 98, 99 for 16 units
+      Wsl[(z >> 1) * WSP + 2 * P + (z & 1)] = 0.f;
+    }
+  }
+  {
+    float hn[2], cn[2], sn[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (MODE == 4) {
+        const float i_ = gate[0][q] * 0.5f, f_ = gate[1][q] * 0.25f, g_ = gate[2][q], o_ = gate[3][q] * 0.5f;
+        cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
+        const float tc = cn[q] * 0.9f;
+        hn[q] = o_ * tc;
+        sn[q] = ((&sa.x)[q] + (&sb.x)[q]) * tc;
+      } else {
+      const float i_ = sigmoidf_(gate[0][q]), f_ = sigmoidf_(gate[1][q]), g_ = tanhf(gate[2][q]),
+                  o_ = sigmoidf_(gate[3][q]);
+      cn[q] = f_ * (&cprev.x)[q] + i_ * g_;
+      const float tc = tanhf(cn[q]);
+      hn[q] = o_ * tc;
+      sn[q] = sigmoidf_((&sa.x)[q] + (&sb.x)[q]) * tc;
+      }
+    }
+    Hs[u0 * HP + rr] = hn[0];
+    Hs[(u0 + 1) * HP + rr] = hn[1];
+    Ss[u0 * HP + rr] = sn[0];
+    Ss[(u0 + 1) * HP + rr] = sn[1];
+    if (m < B) {
+      *reinterpret_cast<float2*>(c_out + (int64_t)m * H + j) = make_float2(cn[0], cn[1]);
+      *reinterpret_cast<float2*>(h_out + (int64_t)m * H + j) = make_float2(hn[0], hn[1]);
+      *reinterpret_cast<float2*>(s_out + (int64_t)m * H + j) = make_float2(sn[0], sn[1]);
+      if (hsp_out && MODE != 6) {
+        // next step's A fragments: k = j.. in chunk nt, lane (m % 32) + 32 * (u0 / 8), elements u0 % 8..
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 p0, p1, p2;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          __bf16 x0, x1, x2;
+          split3(hn[q], x0, x1, x2);
+          p0[q] = x0; p1[q] = x1; p2[q] = x2;
+        }
+        bf16x8* o = hsp_out + ((size_t)((m >> 5) * KC + nt) * 3) * 64 + (m & 31) + 32 * (u0 >> 3);
+        const int e = u0 & 7;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e) = p0;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e) = p1;
+        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e) = p2;
+      }
+    }
+  }
+  if (MODE == 5) return;
+  __syncthreads();
+  // Wave -> one 32x32 block: rows rb*32.., columns cb = 0, 1: W_g j = 0..63; cb = 2, 3: W_s j = 0..63.
+  {
+    const int rb = wave & 1, cb = wave >> 1, li = lane & 31, lh = lane >> 5;
+    const float* X = cb < 2 ? Hs : Ss;
+    const int jj = (cb & 1) * 32 + li, jg = (cb < 2 ? 0 : P) + jj, jgc = jg < WSP ? jg : WSP - 1;
+    floatx16 pacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pacc[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int u = i + 8 * lh;
+      const float av = X[u * HP + rb * 32 + li];
+      const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
+      pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
+    }
+    if (jj < P) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mr = m0 + rb * 32 + acc_row(r, lane);
+        if (mr < B) part[((int64_t)mr * NTn + nt) * PART + jg] = pacc[r];
+      }
+    }
+  }
+}
+
+template <int H, int MODE, class F>
+__device__ __forceinline__ void kv_lgp(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
+                                                   const bf16x8* wf1, float* Pt, F&& between) {
+  constexpr int KC = H / 16, CP = LS_CP, TS = 64 * LS_CP;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
+  const int kc0 = wave * per;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][0][q] = af0[o];
+      fa[slot][1][q] = af1[o];
+      fw[slot][0][q] = wf0[o];
+      fw[slot][1][q] = wf1[o];
+    }
+  };
+  const int last = kc0 + per - 1;
+  asm volatile("" ::: "memory");
+  load(0, kc0);
+  load(1, kc0 + 1 < last ? kc0 + 1 : last);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  between();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < per; i += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) { if (MODE != 1) x3_step(acc[a][c], fa[d][a], fw[d][c]); else acc[a][c][0] += (float)fa[d][a][0][0] * (float)fw[d][c][0][0]; }
+      const int nk = kc0 + i + d + 2;
+      load(d, nk < last ? nk : last);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* dst = Pt + (wave & 3) * TS;
+  const int li = lane & 31, lh = lane >> 5;
+  if (wave >= 4) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[a][c][4 * r4], acc[a][c][4 * r4 + 1], acc[a][c][4 * r4 + 2], acc[a][c][4 * r4 + 3]);
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          float4* e = reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh);
+          const float4 v = *e;
+          *e = make_float4(acc[a][c][4 * r4] + v.x, acc[a][c][4 * r4 + 1] + v.y, acc[a][c][4 * r4 + 2] + v.z,
+                           acc[a][c][4 * r4 + 3] + v.w);
+        }
+  }
+}
+
+template <int H, int MODE, bool G = false>
+__global__ __launch_bounds__(512) void kv_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+                                              const float* __restrict__ table,
+                                              const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
+                                              const float* __restrict__ c_in, const int* __restrict__ par,
+                                              const bf16x8* __restrict__ whh3,
+                                              const float* __restrict__ wgs, float* __restrict__ h_out,
+                                              bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
+                                              float* __restrict__ s_out, float* __restrict__ part) {
+  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
+  __shared__ __attribute__((aligned(16))) float lds[4 * TS + LS_TAIL_FLOATS];
+  constexpr int NTn = H / 16, KC = H / 16;
+  const int MT = (B + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63;
+  const int m0 = mt * BM;
+  float* Pt = lds;  // [4][64][CP] partial tiles
+  const int rr = t >> 3, u0 = (t & 7) * 2, m = m0 + rr;
+  const int mc = m < B ? m : B - 1;  // rows >= B compute on row B-1 and store nothing
+  const int j = nt * 16 + u0;
+  // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
+  //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
+  int64_t tk = tok[(int64_t)mc * tok_ld];
+  const bf16x8* af0;
+  const bf16x8* af1;
+  int pc = mc;  // source row of c (and of h, through the fragments)
+  if constexpr (G) {
+    const int ra0 = m0 + (lane & 31), ra1 = ra0 + 32;
+    const int p0 = par[ra0 < B ? ra0 : B - 1], p1 = par[ra1 < B ? ra1 : B - 1];
+    const int hl = 32 * (lane >> 5);
+    af0 = hsp_in + (size_t)(p0 >> 5) * KC * 3 * 64 + (p0 & 31) + hl;
+    af1 = hsp_in + (size_t)(p1 >> 5) * KC * 3 * 64 + (p1 & 31) + hl;
+    pc = par[mc];
+  } else {
+    af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
+    af1 = af0 + (size_t)KC * 3 * 64;
+  }
+  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
+  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
+  // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
+  float2 ta[4], xa[4], sa, sb, cprev;
+  float4 wsv;
+  kv_lgp<H, MODE>(af0, af1, wf0, wf1, Pt, [&] {
+    tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
+    const int N5 = 5 * H;
+    const float* trow = table + tk * N5;
+    const float* xrow = xg + (int64_t)mc * N5;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
+    }
+    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+    sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
+    cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
+    // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
+    const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
+    wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
+  });
+  if (MODE == 3) { if (t < 64) h_out[(int64_t)(m0 + (t & 63)) * H + nt * 16] = Pt[t] + ta[0].x + xa[0].x + sa.x + sb.x + cprev.x + wsv.x; return; }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
+    const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
+    const float* sp = Pt + cq * CP + r4;
+    float4 v[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
+    float4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
+    *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
+  }
+  __syncthreads();
+  float gate[4][2];
+  {
+    const float* cr = Pt + rr;  // column j of the summed tile at cr[j * CP]
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
+  }
+  if (MODE == 2) { h_out[(int64_t)m * H + j] = gate[0][0] + gate[1][1] + gate[2][0] + gate[3][1] + sa.x + sb.y + cprev.x + wsv.x; return; }
+  kv_tail<H, MODE>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + 4 * TS, h_out, hsp_out, c_out, s_out, part);
+}
+
 // VARIANTS END
 }  // namespace aa
 
@@ -449,6 +702,27 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
     } else if (!strcmp(which, "at_hsfirst")) {
       hipLaunchKernelGGL((kv_at<512, 3>), dim3(B), dim3(512), 0, s, B, 1, w.h[1], w.s, w.part, w.V, w.vwv, p.wh,
                          (float*)nullptr, (int64_t)0, (float*)nullptr, (int64_t)0, w.u, w.ub, w.unorm, (bf16x8*)nullptr);
+    } else if (!strcmp(which, "lstm_m0")) {
+      hipLaunchKernelGGL((kv_lstm<512, 0>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m1")) {
+      hipLaunchKernelGGL((kv_lstm<512, 1>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m2")) {
+      hipLaunchKernelGGL((kv_lstm<512, 2>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m3")) {
+      hipLaunchKernelGGL((kv_lstm<512, 3>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m4")) {
+      hipLaunchKernelGGL((kv_lstm<512, 4>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m5")) {
+      hipLaunchKernelGGL((kv_lstm<512, 5>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m6")) {
+      hipLaunchKernelGGL((kv_lstm<512, 6>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
     // VARIANT LAUNCH END
     } else {
       return false;
