@@ -455,9 +455,10 @@ __device__ __forceinline__ void kv_tail(int B, int m0, int nt, const float (&gat
       const int u = i + 8 * lh;
       const float av = X[u * HP + rb * 32 + li];
       const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
-      pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
+      if (MODE != 7) pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
+      else pacc[i] += av * wv;
     }
-    if (jj < P) {
+    if (jj < P && MODE != 8) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mr = m0 + rb * 32 + acc_row(r, lane);
@@ -628,6 +629,191 @@ __global__ __launch_bounds__(512) void kv_lstm(int B, int V, const int64_t* __re
   kv_tail<H, MODE>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + 4 * TS, h_out, hsp_out, c_out, s_out, part);
 }
 
+template <int NCB, int MODE>
+__global__ __launch_bounds__(512) void kv_enc4(const float* __restrict__ feats, int B, int C,
+                                                const bf16x8* __restrict__ W4, const float* __restrict__ bias,
+                                                float* __restrict__ V, float* __restrict__ a_g) {
+  static_assert(NCB % 2 == 0, "columns are processed in pairs of 16-column blocks");
+  constexpr int H = 128 * NCB, NPAIR = NCB / 2, PL = E4_RB * 16 * E4_LD;  // PL: one plane, bf16
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][PL];
+  __shared__ __attribute__((aligned(16))) float Sg[2][2 * 32 * E4_SP];  // fp32 stage copy for a_g
+  __shared__ __attribute__((aligned(16))) float Ag[2 * E4_MAXC];        // a_g of the two images
+  __shared__ float Junk[MODE >= 3 ? 1024 : 1];
+  const int M = B * P, KC = C / 32;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = blockIdx.x * E4_ROWS;
+  // staging: thread t < 392 -> row r = t % 98, channels 8 kg .. 8 kg + 7 of each 32-channel stage;
+  // threads 392..511 fill garbage rows 98..105 (never stored) from a valid address
+  const int sr = t < 4 * E4_ROWS ? t % E4_ROWS : E4_ROWS + (t & 7);
+  const int kg = t < 4 * E4_ROWS ? t / E4_ROWS : (t >> 3) & 3;
+  int m = m0 + (t < 4 * E4_ROWS ? sr : 0);
+  m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
+  const int bi = m / P, pi = m - bi * P;
+  const float* arow = feats + (int64_t)bi * C * P + pi + (int64_t)(8 * kg) * P;
+  const int so = sr * E4_LD + 8 * kg;
+  // fragment reads: lane l -> row 16 rb + (l & 15), k = 8 (l >> 4)
+  const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);
+  const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;  // block nb = wave NCB + c
+  float ra[8];
+  bf16x8 wv[NCB][3];
+  floatx4 acc[E4_RB][NCB];
+#pragma unroll
+  for (int rb = 0; rb < E4_RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto gload_a = [&](int s) {
+    const float* src = arow + (int64_t)(32 * s) * P;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = src[i * P];
+  };
+  auto gload_w = [&](int s, int c) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)s * 3 + q) * 64];
+  };
+  auto lstore_a = [&](int buf) {
+    bf16x8 x[3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __bf16 x0, x1, x2;
+      split3(ra[i], x0, x1, x2);
+      x[0][i] = x0; x[1][i] = x1; x[2][i] = x2;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&As[buf][q][so]) = x[q];
+    if (MODE >= 3) {  // branch-free: the garbage-row threads write a junk area
+      const int img = sr >= P, pp = sr - img * P;
+      float* g = t < 4 * E4_ROWS ? &Sg[buf][(img * 32 + 8 * kg) * E4_SP + pp] : &Junk[t & 127];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i * (t < 4 * E4_ROWS ? E4_SP : 128)] = ra[i];
+    } else
+    if (MODE != 1 && t < 4 * E4_ROWS) {  // sr = 49 image + p
+      const int img = sr >= P, pp = sr - img * P;
+      float* g = &Sg[buf][(img * 32 + 8 * kg) * E4_SP + pp];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i * E4_SP] = ra[i];
+    }
+  };
+
+  const int ns = KC;
+  gload_a(0);
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) gload_w(0, c);
+  lstore_a(0);
+  gload_a(ns > 1 ? 1 : 0);
+  __syncthreads();
+  for (int s = 0; s < ns; ++s) {
+    const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
+    // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
+    if (MODE < 3) {
+    lstore_a(buf ^ 1);
+    gload_a(s2);
+    __builtin_amdgcn_sched_barrier(0);
+    }
+    const __bf16* Ab = &As[buf][0][fo];
+    if constexpr (MODE == 5 || MODE == 6) {
+      bf16x8 fb[2][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) fb[0][q] = *reinterpret_cast<const bf16x8*>(Ab + q * PL);
+#pragma unroll
+      for (int g = 0; g < NPAIR * E4_RB; ++g) {
+        const int cp = g / E4_RB, rb = g % E4_RB, cur = g & 1;
+        if (g + 1 < NPAIR * E4_RB) {
+          const int rn = (g + 1) % E4_RB;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) fb[cur ^ 1][q] = *reinterpret_cast<const bf16x8*>(Ab + q * PL + rn * 16 * E4_LD);
+        }
+#pragma unroll
+        for (int c = 2 * cp; c < 2 * cp + 2; ++c) {
+          floatx4 x = acc[rb][c];
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][2], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][1], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][0], wv[c][2], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][1], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][0], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][0], wv[c][0], x, 0, 0, 0);
+          acc[rb][c] = x;
+        }
+        if (rb == E4_RB - 1) {
+          gload_w(s1, 2 * cp);
+          gload_w(s1, 2 * cp + 1);
+        }
+        if (MODE == 6 && g == 0) {
+          lstore_a(buf ^ 1);
+          gload_a(s2);
+        }
+      }
+    } else
+#pragma unroll
+    for (int cp = 0; cp < NPAIR; ++cp) {
+#pragma unroll
+      for (int rb = 0; rb < E4_RB; ++rb) {
+        bf16x8 fa[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(Ab + q * PL + rb * 16 * E4_LD);
+#pragma unroll
+        for (int c = 2 * cp; c < 2 * cp + 2; ++c) {
+          floatx4 x = acc[rb][c];
+          if (MODE == 2) { x[0] += (float)fa[2][0] * (float)wv[c][0][1] + (float)fa[0][1] * (float)wv[c][2][3]; acc[rb][c] = x; continue; }
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][2], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][0], x, 0, 0, 0);
+          acc[rb][c] = x;
+        }
+        if (MODE >= 3 && cp == 0 && rb == 0) {
+          lstore_a(buf ^ 1);
+          gload_a(s2);
+        }
+        if (MODE == 4 && cp == 0 && rb == 1) {
+#pragma unroll
+          for (int z = 0; z < 24; ++z) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+          }
+        }
+      }
+      gload_w(s1, 2 * cp);
+      gload_w(s1, 2 * cp + 1);
+      // re-read the A fragments for the next pair instead of keeping all 21 live (VGPR budget)
+      asm volatile("" ::: "memory");
+    }
+    if (MODE != 1 && wave == (s & 7)) {  // a_g of stage s's 32 channels: lane -> (image lane / 32, channel lane % 32)
+      const float* g = &Sg[buf][lane * E4_SP];
+      float sum = 0.f;
+#pragma unroll 4
+      for (int pp = 0; pp < 48; pp += 4) {  // 16-B reads (E4_SP * 4 B = 13 x 16 B), summed in p order
+        const float4 v = *reinterpret_cast<const float4*>(g + pp);
+        sum += v.x; sum += v.y; sum += v.z; sum += v.w;
+      }
+      sum += g[48];
+      Ag[(lane >> 5) * C + 32 * s + (lane & 31)] = sum / 49.0f;
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // a_g of the workgroup's images (the last workgroup of an odd batch holds one)
+  for (int i = t; i < 2 * C; i += 512) {
+    const int img = 2 * blockIdx.x + (i >= C);
+    if (img < B) a_g[(int64_t)img * C + (i - (i >= C ? C : 0))] = Ag[i];
+  }
+  // epilogue: lane l holds column 16 nb + (l & 15), rows 16 rb + 4 (l >> 4) + i
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int col = (wave * NCB + c) * 16 + (lane & 15);
+    const float bv = bias[col];
+#pragma unroll
+    for (int rb = 0; rb < E4_RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rb * 16 + 4 * (lane >> 4) + i, row = m0 + r;
+        if (r < E4_ROWS && row < M) V[(int64_t)row * H + col] = reluf_(acc[rb][c][i] + bv);
+      }
+  }
+}
+
 // VARIANTS END
 }  // namespace aa
 
@@ -723,6 +909,33 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
     } else if (!strcmp(which, "lstm_m6")) {
       hipLaunchKernelGGL((kv_lstm<512, 6>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
                          p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m7")) {
+      hipLaunchKernelGGL((kv_lstm<512, 7>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "lstm_m8")) {
+      hipLaunchKernelGGL((kv_lstm<512, 8>), dim3(MT * (H / 16)), dim3(512), 0, s, B, L.V, (const int64_t*)w.tok0, 1,
+                         p.table, w.xg, w.hsp[0], w.c[0], (const int*)nullptr, p.whh3, p.wgs, w.h[1], w.hsp[1], w.c[1], w.s, w.part);
+    } else if (!strcmp(which, "enc4_m0")) {
+      hipLaunchKernelGGL((kv_enc4<4, 0>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m1")) {
+      hipLaunchKernelGGL((kv_enc4<4, 1>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m2")) {
+      hipLaunchKernelGGL((kv_enc4<4, 2>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m3")) {
+      hipLaunchKernelGGL((kv_enc4<4, 3>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m4")) {
+      hipLaunchKernelGGL((kv_enc4<4, 4>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m5")) {
+      hipLaunchKernelGGL((kv_enc4<4, 5>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
+    } else if (!strcmp(which, "enc4_m6")) {
+      hipLaunchKernelGGL((kv_enc4<4, 6>), dim3((B * P + E4_ROWS - 1) / E4_ROWS), dim3(512), 0, s, feats, B, L.C, p.enc_w4,
+                         p.enc_a_b, w.V, w.a_g);
     // VARIANT LAUNCH END
     } else {
       return false;
