@@ -21,6 +21,7 @@ DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
 DECODE_SCREEN64 = 8
 DECODE_ENC_V3 = 16
+BEAM_TILE128 = 64
 MAX_LANES = 8
 MAX_BEAM = 8
 

@@ -225,6 +225,9 @@ class Encoder2Decoder(nn.Module):
         # True: encoder V GEMM on k_enc_v3 (128 x 128 tiles) instead of k_enc_v4 (two images per
         # workgroup, all columns: the feature map is read once); same accuracy class
         self.enc_v3 = False
+        # True: beam-search vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256 (k_vbeam5);
+        # identical logits
+        self.beam_tile128 = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -411,7 +414,8 @@ class Encoder2Decoder(nn.Module):
             rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
                                     ws.numel() if ws is not None else 0,
-                                    _lib.DECODE_EXACT_VOCAB if exact_vocab else 0, _lib.stream_handle())
+                                    (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0)
+                                    | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle())
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores
 

@@ -342,6 +342,119 @@ __global__ __launch_bounds__(256, 2) void k_vbeam4(int R, int V, int Vp, const b
   }
 }
 
+// k_vbeam5: k_vbeam4's arithmetic and epilogue on 256 x 256 tiles: 16 waves (1024 threads, a 4 x 4
+// grid of 64 x 64 quadrants over the whole K), one workgroup per CU (at R = 1536, Vp = 10240 the
+// grid is 6 x 40 = 240 workgroups: one round, where k_vbeam4's 960 128 x 128 tiles take two rounds
+// of two per CU).  A chunk (one k16 step: 8 A row blocks + 8 W column blocks, 3 planes each = 48
+// fragments = 48 KB) is staged by global_load_lds, three fragments per wave; three stage buffers
+// (144 KB), chunk k + 2 in flight while chunk k is multiplied, so the lead over the L2 / MALL
+// latency is two chunks of 4 waves x 24 MFMAs per SIMD (k_vbeam4: two chunks of 2 x 24).  With
+// four waves per SIMD (128 VGPRs each) a wave holds one fragment set: it reads chunk k from LDS
+// right after the barrier and the other waves' MFMAs cover that latency.
+constexpr int VB5_NBUF = 3, VB5_FR = 48;
+template <int H>
+__global__ __launch_bounds__(1024) void k_vbeam5(int R, int V, int Vp, const bf16x8* __restrict__ ua3,
+                                                 const bf16x8* __restrict__ w3, const float* __restrict__ bias,
+                                                 float* __restrict__ logits, float2* __restrict__ gsum) {
+  constexpr int KC = H / 16;
+  __shared__ __attribute__((aligned(16))) bf16x8 stg[VB5_NBUF][VB5_FR * 64];
+  const int NG = Vp / 32, NTs = Vp / 256, MT = (R + 255) / 256;
+  const int RB = (R + 63) / 64 * 2;  // row blocks present in ua3 (64-row padded)
+  const int L = xcd_remap(blockIdx.x, MT * NTs);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 31, lh = lane >> 5, wr = wave >> 2, wc = wave & 3;
+  const int m0 = mt * 256, n0 = nt * 256;
+  // this wave's 3 fragments of every chunk: f = 3 wave + i; f < 24: A (row block f / 3, plane f % 3)
+  const bf16x8* src[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int f = 3 * wave + i;
+    if (f < 24) {
+      int rb = m0 / 32 + f / 3;
+      rb = rb < RB ? rb : RB - 1;
+      src[i] = ua3 + ((size_t)rb * KC * 3 + f % 3) * 64 + lane;
+    } else {
+      const int cb = n0 / 32 + (f - 24) / 3;
+      src[i] = w3 + ((size_t)cb * KC * 3 + (f - 24) % 3) * 64 + lane;
+    }
+  }
+  auto issue = [&](int kc, int buf) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)kc * 3 * 64),
+                                       (__attribute__((address_space(3))) void*)(&stg[buf][(3 * wave + i) * 64]),
+                                       16, 0, 0);
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  issue(0, 0);
+  if (KC > 1) issue(1, 1);
+  for (int kc = 0; kc < KC; ++kc) {
+    // chunk kc landed (this wave's part: at most chunk kc + 1's three loads still in flight)
+    if (kc + 1 < KC)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everywhere; and every wave has read chunk kc - 1's buffer
+    if (kc + 2 < KC) issue(kc + 2, (kc + 2) % VB5_NBUF);
+    const bf16x8* sb = stg[kc % VB5_NBUF];
+    bf16x8 fa[2][3], fw[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        fa[a][q] = sb[((2 * wr + a) * 3 + q) * 64 + lane];
+        fw[a][q] = sb[(24 + (2 * wc + a) * 3 + q) * 64 + lane];
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[a], fw[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = n0 + wc * 64 + c * 32 + li;
+    const bool valid = col < V;
+    const float bv = bias[col];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      float x[16], m[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[r] = acc[a][c][r] + bv;
+        const int row = m0 + wr * 64 + a * 32 + acc_row(r, lane);
+        if (row < R) logits[(int64_t)row * Vp + col] = x[r];
+        x[r] = valid ? x[r] : -INFINITY;
+        m[r] = x[r];
+      }
+      red_bfly<16, 0>(m, li);
+      red_bfly<8, 0>(m, li);
+      red_bfly<4, 0>(m, li);
+      red_bfly<2, 0>(m, li);
+      const float gmax = fmaxf(m[0], __uint_as_float(partner<1>(__float_as_uint(m[0]))));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float g = __shfl(gmax, 2 * r + 32 * lh, 64);
+        m[r] = valid ? expf(x[r] - g) : 0.f;
+      }
+      red_bfly<16, 1>(m, li);
+      red_bfly<8, 1>(m, li);
+      red_bfly<4, 1>(m, li);
+      red_bfly<2, 1>(m, li);
+      const float gs = m[0] + __uint_as_float(partner<1>(__float_as_uint(m[0])));
+      const int rr = (li >> 1) & 15;
+      const int row = m0 + wr * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = make_float2(gmax, gs);
+    }
+  }
+}
+
 // Selection from the granule summaries: one wave per row (K waves per image).  Row log-sum-exp
 // ls = log(sum_g s_g exp(m_g - M)) (lane-strided granules in order, then the wave tree); the row's
 // top-K tokens lie in the granules whose max reaches the K-th largest granule max (ties kept), so
@@ -575,8 +688,14 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
                          w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {
 #define AA_VB3(H_)                                                                                            \
-  hipLaunchKernelGGL(k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, L.Vp, w.u3,  \
-                     p.mlp_w3, p.mlp_b, w.logits, w.gsum)
+  if (wide)                                                                                                   \
+    hipLaunchKernelGGL(k_vbeam5<H_>, dim3(((R + 255) / 256) * (L.Vp / 256)), dim3(1024), 0, s, R, L.V, L.Vp,     \
+                       w.u3, p.mlp_w3, p.mlp_b, w.logits, w.gsum);                                            \
+  else                                                                                                        \
+    hipLaunchKernelGGL(k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, L.Vp, w.u3, \
+                       p.mlp_w3, p.mlp_b, w.logits, w.gsum)
+      // 256 x 256 tiles when the padded vocabulary is whole 256-column tiles (V = 10,123: 40 of them)
+      const bool wide = L.Vp % 256 == 0 && !(flags & AA_BEAM_TILE128);
       switch (H) {
         case 256: AA_VB3(256); break;
         case 512: AA_VB3(512); break;

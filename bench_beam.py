@@ -56,10 +56,13 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tile128", action="store_true", help="vocab logits on 128x128 tiles (k_vbeam4) instead of "
+                    "256x256 (k_vbeam5)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, K, T = args.batch, args.beam, args.T
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    model.beam_tile128 = args.tile128
     feats = synthetic_features(B, dev, seed=0)
     for _ in range(args.warmup):
         model.beam_search(feats, T, K)
@@ -74,7 +77,8 @@ def main():
            "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": "fp32",
            "data": "synthetic: U[0,1) post-trunk features, random-init weights (adaptive_amd.synth seed 123)",
            "config": {"workload": f"Encoder2Decoder.beam_search B={B} beam={K} max_len={T}", "batch": B,
-                      "beam": K, "T": T, "rows": B * K},
+                      "beam": K, "T": T, "rows": B * K,
+                      "vocab_kernel": "k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"},
            "best_score_mean": float(out[4][:, 0].mean().item()), "cpu_baseline": None}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(K, T, args.cpu_sample, args.cpu_budget)

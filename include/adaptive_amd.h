@@ -183,6 +183,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
                                   (k_lstm) instead of the split k_lstm_gemm + k_lstm_cell */
 #define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of
                                     the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v4) */
+#define AA_BEAM_TILE128 64 /* beam search: vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256
+                             (k_vbeam5); identical logits */
 #define AA_DECODE_ENC_V3 16 /* V on the 128 x 128-tile bf16x3 kernel (k_enc_v3) instead of k_enc_v4 (one
                                workgroup per two images, all H columns; H in {256, 512}) */
 

@@ -86,6 +86,21 @@ def test_beam_bf16x3_logits_match_fp32(gpu_device):
     torch.testing.assert_close(a[4][same], b[4][same], atol=SCORE_TOL, rtol=0)
 
 
+def test_beam_tile256_equals_tile128(gpu_device):
+    """k_vbeam5 (256 x 256 tiles, the default when the padded vocabulary is whole 256-column tiles)
+    and k_vbeam4 (128 x 128) run the same per-element product order: bit-identical beams."""
+    m = _model(gpu_device, _weights(end_boost=2.6))
+    f = torch.from_numpy(synth.make_features(200, seed=8)).to(gpu_device)
+    a = m.beam_search(f, 12, 3)
+    m.beam_tile128 = True
+    try:
+        b = m.beam_search(f, 12, 3)
+    finally:
+        m.beam_tile128 = False
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_beam_batch_invariance(gpu_device):
     """An image's beams do not depend on the rest of the batch (bit-exact)."""
     m = _model(gpu_device, _weights(end_boost=2.6))
