@@ -15,13 +15,14 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
 DECODE_SCREEN64 = 8
 DECODE_ENC_V3 = 16
 BEAM_TILE128 = 64
+TRAIN_BF16 = 128
 MAX_LANES = 8
 MAX_BEAM = 8
 
@@ -99,10 +100,10 @@ SIGNATURES = {
     "aa_decode_plan_destroy": (c_int, [c_void_p]),
     "aa_train_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
     "aa_train_forward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p, c_int32,
-                                 c_void_p, c_void_p, c_int32, c_void_p, c_size_t, c_void_p]),
+                                 c_void_p, c_void_p, c_int32, c_void_p, c_size_t, c_int32, c_void_p]),
     "aa_train_backward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p, c_int32,
                                   c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_void_p, c_size_t,
-                                  c_void_p]),
+                                  c_int32, c_void_p]),
     "aa_beam_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32, c_int32]),
     "aa_beam_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p]),

@@ -228,6 +228,9 @@ class Encoder2Decoder(nn.Module):
         # True: beam-search vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256 (k_vbeam5);
         # identical logits
         self.beam_tile128 = False
+        # True: teacher-forced training (forward()) with every GEMM on bf16 MFMA (bf16 operands, fp32
+        # accumulation: BASELINE config 5); False: fp32 GEMMs
+        self.train_bf16 = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -427,6 +430,9 @@ class Encoder2Decoder(nn.Module):
             cache[key] = torch.cuda.Stream(device=dev)
         return cache[key]
 
+    def _train_flags(self) -> int:
+        return _lib.TRAIN_BF16 if getattr(self, "train_bf16", False) else 0
+
     def _lstm_flags(self) -> int:
         return ((0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
                 | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0))
@@ -574,9 +580,9 @@ class _TeacherForced(torch.autograd.Function):
         with torch.cuda.device(images.device):
             rc = lib.aa_train_forward(w, d, images.data_ptr(), B, T, caps.data_ptr(), caps.stride(0),
                                       len_dev.data_ptr(), scores.data_ptr(), N, ws.data_ptr(), nbytes,
-                                      _lib.stream_handle())
+                                      owner._train_flags(), _lib.stream_handle())
         _lib.check(rc, "train_forward")
-        ctx.owner, ctx.ws, ctx.N, ctx.T = owner, ws, N, T
+        ctx.owner, ctx.ws, ctx.N, ctx.T, ctx.flags = owner, ws, N, T, owner._train_flags()
         ctx.save_for_backward(images, caps, len_dev, *params)
         return scores
 
@@ -594,7 +600,7 @@ class _TeacherForced(torch.autograd.Function):
         with torch.cuda.device(images.device):
             rc = lib.aa_train_backward(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(), caps.stride(0),
                                        len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g, _lib.ptr(dfeats),
-                                       ctx.ws.data_ptr(), ctx.ws.numel(), _lib.stream_handle())
+                                       ctx.ws.data_ptr(), ctx.ws.numel(), ctx.flags, _lib.stream_handle())
         _lib.check(rc, "train_backward")
         ctx.ws = None
         return (None, dfeats, None, None, None, None, *grads)

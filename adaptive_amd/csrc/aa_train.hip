@@ -8,7 +8,8 @@
 // works on rows [tB, (t+1)B) and pack_padded_sequence's packed rows (t-major over b < batch
 // size of t; lengths sorted descending) are a monotone subset of the rows.
 //
-// Arithmetic: fp32 throughout.  GEMMs run on the generic fp32-MFMA tile kernel k_tgemm below
+// Arithmetic: fp32 throughout (with AA_TRAIN_BF16 the GEMMs take bf16 operands, fp32 accumulation).
+// GEMMs run on the generic MFMA tile kernel k_tgemm below
 // (operands in any of the layouts the backward pass needs, bounds-checked, fixed accumulation
 // order); everything else is elementwise or one-workgroup-per-row / per-image kernels with fixed
 // reduction orders, so a training step is deterministic run to run.  The cross-entropy loss is
@@ -48,6 +49,14 @@ struct TG {
   float* part;
 };
 
+// bf16 operand tiles (AA_TRAIN_BF16): [64 rows][LDB] per operand, k contiguous; a row pitch of
+// 80 B makes the 16-B fragment reads (lane = row + 32 * k-half) conflict-free
+constexpr int LDB = BK + 8;
+
+// BF: operands rounded to bf16 (RNE) as they are staged in LDS, products on
+// v_mfma_f32_32x32x16_bf16 with fp32 accumulation (BASELINE config 5: bf16 compute, fp32 master
+// weights); same tiles, loads, k order of the partial sums and epilogue as the fp32 engine.
+template <bool BF>
 __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][64 * LDK];
   const int tilesN = (g.N + 63) / 64;
@@ -119,6 +128,33 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
     }
   };
   auto lstore = [&](int buf) {
+    if constexpr (BF) {
+      __bf16* As = reinterpret_cast<__bf16*>(lds[buf][0]);
+      __bf16* Ws = reinterpret_cast<__bf16*>(lds[buf][1]);
+      if (!g.at) {
+        const int r = t >> 2, kq = (t & 3) * 8;
+        bf16x8 v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (__bf16)ra[i];
+        *reinterpret_cast<bf16x8*>(As + r * LDB + kq) = v;
+      } else {
+        const int k = t >> 3, mq = (t & 7) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) As[(mq + i) * LDB + k] = (__bf16)ra[i];
+      }
+      if (g.wm == 1) {
+        const int k = t >> 3, nq = (t & 7) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Ws[(nq + i) * LDB + k] = (__bf16)rw[i];
+      } else {
+        const int r = t >> 2, kq = (t & 3) * 8;
+        bf16x8 v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (__bf16)rw[i];
+        *reinterpret_cast<bf16x8*>(Ws + r * LDB + kq) = v;
+      }
+      return;
+    }
     float* As = lds[buf][0];
     float* Ws = lds[buf][1];
     if (!g.at) {
@@ -150,14 +186,25 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nk) gload(kbeg + (ks + 1) * BK);
-    const float* As = lds[buf][0];
-    const float* Ws = lds[buf][1];
+    if constexpr (BF) {
+      const __bf16* As = reinterpret_cast<const __bf16*>(lds[buf][0]);
+      const __bf16* Ws = reinterpret_cast<const __bf16*>(lds[buf][1]);
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const float4 a = *reinterpret_cast<const float4*>(As + (wmv * 32 + li) * LDK + 16 * lh + 4 * s4);
-      const float4 w = *reinterpret_cast<const float4*>(Ws + (wnv * 32 + li) * LDK + 16 * lh + 4 * s4);
+      for (int kb = 0; kb < 2; ++kb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (wmv * 32 + li) * LDB + 16 * kb + 8 * lh);
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(Ws + (wnv * 32 + li) * LDB + 16 * kb + 8 * lh);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w, acc, 0, 0, 0);
+      }
+    } else {
+      const float* As = lds[buf][0];
+      const float* Ws = lds[buf][1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a, j), f4c(w, j), acc, 0, 0, 0);
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const float4 a = *reinterpret_cast<const float4*>(As + (wmv * 32 + li) * LDK + 16 * lh + 4 * s4);
+        const float4 w = *reinterpret_cast<const float4*>(Ws + (wnv * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a, j), f4c(w, j), acc, 0, 0, 0);
+      }
     }
     if (ks + 1 < nk) lstore(buf ^ 1);
     __syncthreads();
@@ -205,6 +252,7 @@ struct GemmCtx {
   hipStream_t s;
   float* split;
   size_t cap;  // floats
+  bool bf16;   // AA_TRAIN_BF16: bf16 operands, fp32 accumulation
 };
 
 // C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites.  GEMMs with
@@ -231,7 +279,10 @@ static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_
   }
   TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, splits, kper,
        splits > 1 ? gc.split : nullptr};
-  hipLaunchKernelGGL(k_tgemm, dim3(tiles * splits), dim3(256), 0, s, g);
+  if (gc.bf16)
+    hipLaunchKernelGGL(k_tgemm<true>, dim3(tiles * splits), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(k_tgemm<false>, dim3(tiles * splits), dim3(256), 0, s, g);
   if (splits > 1)
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
 }
@@ -746,7 +797,7 @@ static inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs
 
 int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
                      const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, float* scores, int32_t N,
-                     void* workspace, size_t workspace_bytes, aa_stream_t stream) {
+                     void* workspace, size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
   using namespace aa;
   int rc = train_check(dims, B, T);
   if (rc) return rc;
@@ -758,7 +809,7 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
   // encoder tail (baseline_attention.py:46-60), reference weight layouts
   hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
   {
@@ -802,7 +853,7 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
 int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
                       const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, const float* dscores, int32_t N,
                       const aa_ref_grads* grads, float* dfeats, void* workspace, size_t workspace_bytes,
-                      aa_stream_t stream) {
+                      int32_t flags, aa_stream_t stream) {
   using namespace aa;
   int rc = train_check(dims, B, T);
   if (rc) return rc;
@@ -814,7 +865,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B, E2 = 2 * E;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
 #define GRAD(f) (grads->f)
   const size_t RH = (size_t)R * H;
   // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)

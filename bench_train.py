@@ -6,7 +6,8 @@ of Encoder2Decoder at B=128, captions of T=18 steps (+ <start>), on 1 MI355X:
     -> backward (HIP) -> clip_grad_norm_(LSTM, 5) -> Adam step          (train.py:197-219)
 
 Synthetic data: post-trunk features [B,2048,7,7] U[0,1), random captions with lengths 18 .. 9
-sorted descending, random-init weights of the reference architecture.  fp32 compute.  Prints ONE
+sorted descending, random-init weights of the reference architecture.  bf16 GEMMs (fp32 accumulate,
+fp32 master weights and elementwise work; BASELINE config 5) by default, --dtype fp32 for fp32 GEMMs.  Prints ONE
 JSON line (steps/s; ms/step; the CPU oracle's autograd step timed on this host beside it).
 
     python bench_train.py [--steps 20] [--warmup 3] [--batch 128] [--T 18] [--no-cpu-baseline]
@@ -83,11 +84,14 @@ def main():
     ap.add_argument("--T", type=int, default=18)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="GEMM operand type: bf16 (AA_TRAIN_BF16, BASELINE config 5) or fp32")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, T = args.batch, args.T
     caps_np, lengths = make_batch(B, T)
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    model.train_bf16 = args.dtype == "bf16"
     feats = synthetic_features(B, dev, seed=0)
     caps = torch.from_numpy(caps_np).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
@@ -101,10 +105,12 @@ def main():
     el = time.perf_counter() - t0
     out = {"metric": "training steps/s (teacher-forced fwd+bwd+Adam, B=128, T=18)", "value": args.steps / el,
            "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": "fp32",
+           "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": args.dtype,
            "data": "synthetic: U[0,1) post-trunk features, random captions (lengths T..T/2, sorted), random-init weights",
            "config": {"workload": f"Encoder2Decoder.forward + CE + backward + clip + Adam, B={B}, T={T}",
-                      "batch": B, "T": T, "packed_rows": int(sum(lengths))},
+                      "batch": B, "T": T, "packed_rows": int(sum(lengths)),
+                      "gemm": "bf16 operands, fp32 accumulate (v_mfma_f32_32x32x16_bf16), fp32 master weights / Adam"
+                      if args.dtype == "bf16" else "fp32 (v_mfma_f32_32x32x2f32)"},
            "final_loss": float(loss.item()), "cpu_baseline": None}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(caps_np, lengths, B, args.cpu_budget)

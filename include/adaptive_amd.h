@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 9
+#define AA_ABI_VERSION 10
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -253,15 +253,19 @@ AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
  * dL/dfeats [B,C,7,7] (the gradient into the ResNet trunk's output, for CNN fine-tuning).  The reference's loss
  * (train.py: CrossEntropyLoss on the packed scores) stays with the caller. */
 AA_API size_t aa_train_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
+#define AA_TRAIN_BF16 128 /* aa_train_forward / aa_train_backward flags: every GEMM on bf16 MFMA
+                               (operands rounded to bf16, fp32 accumulation; BASELINE config 5's
+                               "bf16 compute / fp32 master"); elementwise work and the encoder V GEMM
+                               stay fp32.  0 = fp32 GEMMs (fp32 MFMA).  Pass the same flags to both. */
 AA_API int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B,
                             int32_t T, const int64_t* tokens, int32_t tok_ld, const int32_t* lengths,
                             float* scores, int32_t N, void* workspace, size_t workspace_bytes,
-                            aa_stream_t stream);
+                            int32_t flags, aa_stream_t stream);
 AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float* feats,
                              int32_t B, int32_t T, const int64_t* tokens, int32_t tok_ld,
                              const int32_t* lengths, const float* dscores, int32_t N,
                              const aa_ref_grads* grads, float* dfeats, void* workspace,
-                             size_t workspace_bytes, aa_stream_t stream);
+                             size_t workspace_bytes, int32_t flags, aa_stream_t stream);
 
 /* ---- beam-search decode (BASELINE config 4) ------------------------------
  * Not in the reference (its for_wzn:3 lists beam search as a TODO): semantics defined here and in

@@ -150,3 +150,75 @@ def test_train_closure_adam_clip_reduces_loss(gpu_device):
         torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
         opt.step()
     assert losses[-1] < losses[0]
+
+
+# bf16 GEMMs (AA_TRAIN_BF16, BASELINE config 5 "bf16 compute / fp32 master"): every GEMM operand is
+# rounded to bf16 (unit roundoff 2^-8 = 3.9e-3) with fp32 accumulation, so a product carries a
+# relative error of ~2 * 3.9e-3 / sqrt(averaging) per GEMM and the chain forward -> backward
+# compounds a few of them.  Tolerances: packed scores within 2e-2 relative (Frobenius) of the fp32
+# oracle, the loss within 1e-3 relative, each parameter gradient within 5e-2 relative (Frobenius).
+BF16_SCORE_REL = 2e-2
+BF16_LOSS_REL = 1e-3
+BF16_GRAD_REL = 5e-2
+
+
+def test_train_bf16_vs_oracle(gpu_device):
+    from oracle.adaptive_oracle import TrainOracle
+    B, L = 13, 12
+    lengths = [9, 9, 8, 7, 7, 6, 5, 4, 4, 3, 2, 1, 1]
+    rng = np.random.default_rng(5)
+    caps_np = rng.integers(0, 10123, size=(B, L)).astype(np.int64)
+    caps_np[:, 0] = 1
+    state = synth.make_weights(31, bias_noise=0.01)
+    feats_np = synth.make_features(B, seed=9)
+    oracle = TrainOracle(state)
+    rloss, rpacked = oracle.loss(torch.from_numpy(feats_np), torch.from_numpy(caps_np), lengths)
+    rloss.backward()
+    model = _model(gpu_device, seed=31, noise=0.01)
+    model.train_bf16 = True
+    loss, packed = _loss(model, torch.from_numpy(feats_np).to(gpu_device), torch.from_numpy(caps_np).to(gpu_device),
+                         lengths)
+    got = packed[0].detach().cpu().double().numpy()
+    ref = rpacked[0].detach().double().numpy()
+    assert np.linalg.norm(got - ref) <= BF16_SCORE_REL * np.linalg.norm(ref)
+    assert abs(loss.item() - rloss.item()) <= BF16_LOSS_REL * abs(rloss.item())
+    loss.backward()
+    for k, p in model.named_parameters():
+        g = p.grad.detach().cpu().double().numpy()
+        r = oracle.w[k].grad.detach().double().numpy()
+        assert np.linalg.norm(g - r) <= BF16_GRAD_REL * max(np.linalg.norm(r), 1e-30), k
+    # and the bf16 run really differs from the fp32 engine (the flag reaches the kernels)
+    model.train_bf16 = False
+    _, p32 = _loss(model, torch.from_numpy(feats_np).to(gpu_device), torch.from_numpy(caps_np).to(gpu_device),
+                   lengths)
+    assert not torch.equal(p32[0].detach(), packed[0].detach())
+
+
+def test_train_bf16_deterministic_and_reduces_loss(gpu_device):
+    B, L = 8, 10
+    lengths = [9, 8, 8, 6, 5, 5, 3, 2]
+    rng = np.random.default_rng(11)
+    caps = torch.from_numpy(rng.integers(0, 10123, size=(B, L)).astype(np.int64)).to(gpu_device)
+    caps[:, 0] = 1
+    feats = torch.from_numpy(synth.make_features(B, seed=3)).to(gpu_device)
+    grads = []
+    for _ in range(2):
+        model = _model(gpu_device)
+        model.train_bf16 = True
+        loss, _ = _loss(model, feats, caps, lengths)
+        loss.backward()
+        grads.append({k: p.grad.clone() for k, p in model.named_parameters()})
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+    model = _model(gpu_device)
+    model.train_bf16 = True
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(5):
+        opt.zero_grad()
+        loss, _ = _loss(model, feats, caps, lengths)
+        losses.append(loss.item())
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+        opt.step()
+    assert losses[-1] < losses[0]
