@@ -440,15 +440,18 @@ __global__ void k_tr_prow(const int* __restrict__ len, int B, int T, int* __rest
 // ---------------------------------------------------------------------------------------------
 // backward pieces
 // ---------------------------------------------------------------------------------------------
-// Atten backward, one workgroup per image b over its steps t < len[b] in order (rows t >= len[b]
-// carry no loss gradient), 256 threads, HPT = H / 256 columns per thread.
+// Atten backward, one workgroup per (image b, step group g) over the steps t in
+// [g TS, min((g+1) TS, len[b])) in order (rows t >= len[b] carry no loss gradient), 256 threads,
+// HPT = H / 256 columns per thread.  With more than one group each group writes its own partial
+// dV / dVWv / dwh (strides sV, sVW, swh) and k_sum_groups adds them in group order.
 // In: dU (= dc_hat; u = c_hat + h also gives dh = dU directly), alpha, beta, ctx (c_t), S, PG,
 // PS, VWv, V, w_h.  Out per row: dS = beta dU, dPG, dPS (pitch PP); per image: dV[b] (+)= sum_t
 // alpha_t (x) dc_t, dVWv[b] = sum_t dcontent_v, dwh_part[b][j].
 //   beta = softmax_50([z; z_s])[49]:  dz_k += -dbeta beta (1 - beta) alpha_k, dz_s = dbeta beta (1 - beta)
 //   alpha = softmax_49(z):           dz_k += alpha_k (dalpha_k - <alpha, dalpha>)
 template <int HPT>
-__global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restrict__ len, const float* __restrict__ dU,
+__global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, int TS, int64_t sV, int64_t sVW, int64_t swh,
+                                                      const int* __restrict__ len, const float* __restrict__ dU,
                                                       const float* __restrict__ alpha, const float* __restrict__ beta,
                                                       const float* __restrict__ ctx, const float* __restrict__ S,
                                                       const float* __restrict__ PG, const float* __restrict__ PS,
@@ -473,8 +476,11 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
   for (int i = 0; i < 10; ++i) dvwv_acc[i] = 0.f;
   float dwh_acc = 0.f;
   const float whj = t < P ? wh[t] : 0.f;
-  const int nt = len[b];
-  for (int tt = 0; tt < nt; ++tt) {
+  const int g = blockIdx.y, nt = min(len[b], (g + 1) * TS);
+  dV += g * sV;
+  dVWv += g * sVW;
+  dwh_part += g * swh;
+  for (int tt = g * TS; tt < nt; ++tt) {
     const int r = tt * B + b;
     const float be = beta[r];
     float part = 0.f;
@@ -555,6 +561,15 @@ __global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, const int* __restri
     if (e < P * P) dVWv[((int64_t)b * P + e / P) * PP + e % P] = dvwv_acc[i];
   }
   if (t < P) dwh_part[(int64_t)b * PP + t] = dwh_acc;
+}
+
+// out[i] = sum over g of parts[g n + i], in g order
+__global__ void k_sum_groups(const float* __restrict__ parts, int G, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = parts[i];
+  for (int g = 1; g < G; ++g) v += parts[g * n + i];
+  out[i] = v;
 }
 
 // copy a [rows][cols] matrix into pitch `pitch` (zero padding)
@@ -721,8 +736,18 @@ struct TrainWS {
   // backward scratch
   float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
   float *dA, *dag;  // d(features) pieces: through V [B*49][C] and through a_g [B][C]
+  float *pV, *pVWv, *pwh;  // per-step-group partials of k_tr_atten_bwd (atb_groups > 1)
   int *trank, *tcount, *torder, *tsmall;
 };
+
+// step groups of k_tr_atten_bwd: enough (image, group) workgroups to cover the chip at small B
+static void atb_groups(int B, int T, int* G, int* TS) {
+  int g = B > 0 ? (512 + B - 1) / B : 1;
+  g = g < T ? g : T;
+  g = g > 1 ? g : 1;
+  *TS = (T + g - 1) / g;
+  *G = *TS > 0 ? (T + *TS - 1) / *TS : 1;
+}
 
 static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax, size_t* bytes) {
   Carver c{base};
@@ -774,6 +799,12 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.tcount = c.take<int>(R);
   w.torder = c.take<int>(R);
   w.tsmall = c.take<int>(R);
+  int G, TS;
+  atb_groups(B, T, &G, &TS);
+  const size_t np = G > 1 ? (size_t)G : 0;
+  w.pV = c.take<float>(np * B * P_ * H);
+  w.pVWv = c.take<float>(np * B * P_ * PP_);
+  w.pwh = c.take<float>(np * B * PP_);
   *bytes = c.off;
   return w;
 }
@@ -880,9 +911,15 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
   AA_TRY(hipMemsetAsync(s.dPG, 0, sizeof(float) * (size_t)R * PP, st));
   AA_TRY(hipMemsetAsync(s.dPS, 0, sizeof(float) * (size_t)R * PP, st));
+  int G, TS;
+  atb_groups(B, T, &G, &TS);
+  const bool grouped = G > 1;
+  const int64_t nV = (int64_t)B * P * H, nVW = (int64_t)B * P * PP, nwh = (int64_t)B * PP;
 #define AA_ATB(HPT_)                                                                                          \
-  hipLaunchKernelGGL(k_tr_atten_bwd<HPT_>, dim3(B), dim3(256), 0, st, B, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, \
-                     s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, s.dV, s.dVWv, s.dwh)
+  hipLaunchKernelGGL(k_tr_atten_bwd<HPT_>, dim3(B, G), dim3(256), 0, st, B, TS, grouped ? nV : 0,              \
+                     grouped ? nVW : 0, grouped ? nwh : 0, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, s.PG, s.PS, \
+                     s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, grouped ? s.pV : s.dV,                   \
+                     grouped ? s.pVWv : s.dVWv, grouped ? s.pwh : s.dwh)
   switch (H / 256) {
     case 1: AA_ATB(1); break;
     case 2: AA_ATB(2); break;
@@ -890,6 +927,11 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     default: AA_ATB(4); break;
   }
 #undef AA_ATB
+  if (grouped) {
+    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nV)), dim3(256), 0, st, s.pV, G, nV, s.dV);
+    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nVW)), dim3(256), 0, st, s.pVWv, G, nVW, s.dVWv);
+    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nwh)), dim3(256), 0, st, s.pwh, G, nwh, s.dwh);
+  }
   AA_TRY(hipMemcpyAsync(s.dH, s.dU, sizeof(float) * RH, hipMemcpyDeviceToDevice, st));  // u = c_hat + h
   tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
   tgemm(gc, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
