@@ -130,7 +130,7 @@ def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=512, help="images per GPU")
     ap.add_argument("--max-len", type=int, default=20)
@@ -141,7 +141,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch kernels directly instead of replaying the "
                     "captured decode plan (hipGraph)")
     ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
-    ap.add_argument("--pipeline-depth", type=int, default=2, help="batches in flight in the headline region "
+    ap.add_argument("--pipeline-depth", type=int, default=4, help="batches in flight in the headline region "
                     "(adaptive_amd.pipeline.DecodePipeline: batch i+1 starts on its own stream while batch i "
                     "finishes); 1 = one sampler() call after another")
     ap.add_argument("--split-lstm", action="store_true", help="split LSTM steps: k_lstm_gemm on a side stream "
