@@ -25,8 +25,8 @@ namespace aa {
 //             wm == 2 : NCHW feature map [B][C][49] read as the [B*49, C] row matrix transposed:
 //                       W(n = c, k = b*49 + p) = W[b*ldw*49 + c*49 + p]   (ldw = C)
 //   C row m -> crow ? crow[m] : m
-// 64x64 tiles, 256 threads (2 x 2 waves of 32x32), BK = 32 through double-buffered LDS, the same
-// k order as aa_gemm.hpp (lanes 0-31: k = s, lanes 32-63: k = 16 + s of each step).
+// 64x64 tiles, 256 threads (2 x 2 waves of 32x32), K steps of TStep::KS through double-buffered LDS
+// (fp32 MFMA: lanes 0-31 take k = s, lanes 32-63 k = KS/2 + s of each step).
 // ---------------------------------------------------------------------------------------------
 struct TG {
   int M, N, K;
@@ -45,20 +45,28 @@ struct TG {
   int accumulate;
   int act;      // 0 none, 1 relu, 2 tanh
   int splits;   // split-K: > 1 -> raw partial tiles to part[split][M][N], reduced by k_tgemm_reduce
-  int kper;     // K per split (multiple of BK)
+  int kper;     // K per split (multiple of the K step)
   float* part;
 };
 
-// bf16 operand tiles (AA_TRAIN_BF16): [64 rows][LDB] per operand, k contiguous; a row pitch of
-// 80 B makes the 16-B fragment reads (lane = row + 32 * k-half) conflict-free
-constexpr int LDB = BK + 8;
+// K step of the training GEMM: 64 with bf16 operands (two 32-wide halves per thread, so a
+// latency-bound GEMM -- the per-step recurrent ones, K = 128 per split -- pays half the global round
+// trips), 32 with fp32 operands (a 64-deep fp32 tile pair would need 70 KB of LDS and halve the
+// occupancy of the large GEMMs: measured slower).  Tiles [64 rows][pitch]: fp32 pitch KS + 4 floats,
+// bf16 KS + 8 bf16 (conflict-free 16-B fragment reads either way).
+template <bool BF>
+struct TStep {
+  static constexpr int KS = BF ? 64 : 32, HH = KS / 32, LDK = KS + 4, LDB = KS + 8;
+  static constexpr int TILE_F = BF ? 64 * LDB / 2 : 64 * LDK;  // one operand tile, in floats
+};
 
 // BF: operands rounded to bf16 (RNE) as they are staged in LDS, products on
 // v_mfma_f32_32x32x16_bf16 with fp32 accumulation (BASELINE config 5: bf16 compute, fp32 master
-// weights); same tiles, loads, k order of the partial sums and epilogue as the fp32 engine.
+// weights); same tiles, loads and epilogue as the fp32 engine.
 template <bool BF>
 __global__ __launch_bounds__(256) void k_tgemm(TG g) {
-  __shared__ __attribute__((aligned(16))) float lds[2][2][64 * LDK];
+  constexpr int TBK = TStep<BF>::KS, HH = TStep<BF>::HH, TLDK = TStep<BF>::LDK, TLDB = TStep<BF>::LDB;
+  __shared__ __attribute__((aligned(16))) float lds[2][2][TStep<BF>::TILE_F];
   const int tilesN = (g.N + 63) / 64;
   const int split = blockIdx.x % g.splits, tile = blockIdx.x / g.splits;
   const int mt = tile / tilesN, nt = tile % tilesN;
@@ -66,142 +74,144 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   const int m0 = mt * 64, n0 = nt * 64;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wmv = wave >> 1, wnv = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  float ra[8], rw[8];
+  float ra[HH][8], rw[HH][8];  // [32-wide k half][8 consecutive elements]
   // operands are read 8 consecutive elements per thread along their contiguous dimension, as two
   // 16-B loads when the 8 are in bounds and aligned, else element by element with zero fill
   const bool a4 = ((g.lda & 3) == 0) && ((((uintptr_t)g.A) & 15) == 0);
   const bool w4 = ((g.ldw & 3) == 0) && ((((uintptr_t)g.W) & 15) == 0) && g.wm != 2;
-  auto load8 = [&](float (&r)[8], const float* base, bool fast) {
-    if (fast) {
-      const float4 x = *reinterpret_cast<const float4*>(base), y = *reinterpret_cast<const float4*>(base + 4);
-      r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w; r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
-    }
+  auto load8 = [&](float (&r)[8], const float* base) {
+    const float4 x = *reinterpret_cast<const float4*>(base), y = *reinterpret_cast<const float4*>(base + 4);
+    r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w; r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
   };
   auto gload = [&](int k0) {
-    if (!g.at) {  // 4 threads per row, 8 consecutive k each
-      const int r = t >> 2, kq = (t & 3) * 8, m = m0 + r;
-      const int64_t base = (int64_t)(m < g.M ? (g.arow ? g.arow[m] : m) : 0) * g.lda;
-      const bool fast = a4 && m < g.M && k0 + kq + 8 <= kend;
-      if (fast) load8(ra, g.A + base + k0 + kq, true);
-      else
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k = k0 + kq + i;
-          ra[i] = (m < g.M && k < kend) ? g.A[base + k] : 0.f;
-        }
-    } else {  // 8 threads per k, 8 consecutive m each
-      const int k = k0 + (t >> 3), mq = (t & 7) * 8;
-      const bool fast = a4 && k < kend && m0 + mq + 8 <= g.M;
-      if (fast) load8(ra, g.A + (int64_t)k * g.lda + m0 + mq, true);
-      else
+    for (int hh = 0; hh < HH; ++hh) {
+      const int kh = k0 + 32 * hh;
+      if (!g.at) {  // 4 threads per row, 8 consecutive k each
+        const int r = t >> 2, kq = (t & 3) * 8, m = m0 + r;
+        const int64_t base = (int64_t)(m < g.M ? (g.arow ? g.arow[m] : m) : 0) * g.lda;
+        if (a4 && m < g.M && kh + kq + 8 <= kend) load8(ra[hh], g.A + base + kh + kq);
+        else
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int m = m0 + mq + i;
-          ra[i] = (m < g.M && k < kend) ? g.A[(int64_t)k * g.lda + m] : 0.f;
-        }
-    }
-    if (g.wm == 1) {
-      const int k = k0 + (t >> 3), nq = (t & 7) * 8;
-      const bool fast = w4 && k < kend && n0 + nq + 8 <= g.N;
-      if (fast) load8(rw, g.W + (int64_t)k * g.ldw + n0 + nq, true);
-      else
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int n = n0 + nq + i;
-          rw[i] = (n < g.N && k < kend) ? g.W[(int64_t)k * g.ldw + n] : 0.f;
-        }
-    } else {
-      const int r = t >> 2, kq = (t & 3) * 8, n = n0 + r;
-      const bool fast = w4 && n < g.N && k0 + kq + 8 <= kend;
-      if (fast) load8(rw, g.W + (int64_t)n * g.ldw + k0 + kq, true);
-      else
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k = k0 + kq + i;
-          float v = 0.f;
-          if (n < g.N && k < kend) {
-            if (g.wm == 0) v = g.W[(int64_t)n * g.ldw + k];
-            else v = g.W[((int64_t)(k / P) * g.ldw + n) * P + (k % P)];
+          for (int i = 0; i < 8; ++i) {
+            const int k = kh + kq + i;
+            ra[hh][i] = (m < g.M && k < kend) ? g.A[base + k] : 0.f;
           }
-          rw[i] = v;
-        }
+      } else {  // 8 threads per k, 8 consecutive m each
+        const int k = kh + (t >> 3), mq = (t & 7) * 8;
+        if (a4 && k < kend && m0 + mq + 8 <= g.M) load8(ra[hh], g.A + (int64_t)k * g.lda + m0 + mq);
+        else
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int m = m0 + mq + i;
+            ra[hh][i] = (m < g.M && k < kend) ? g.A[(int64_t)k * g.lda + m] : 0.f;
+          }
+      }
+      if (g.wm == 1) {
+        const int k = kh + (t >> 3), nq = (t & 7) * 8;
+        if (w4 && k < kend && n0 + nq + 8 <= g.N) load8(rw[hh], g.W + (int64_t)k * g.ldw + n0 + nq);
+        else
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int n = n0 + nq + i;
+            rw[hh][i] = (n < g.N && k < kend) ? g.W[(int64_t)k * g.ldw + n] : 0.f;
+          }
+      } else {
+        const int r = t >> 2, kq = (t & 3) * 8, n = n0 + r;
+        if (w4 && n < g.N && kh + kq + 8 <= kend) load8(rw[hh], g.W + (int64_t)n * g.ldw + kh + kq);
+        else
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k = kh + kq + i;
+            float v = 0.f;
+            if (n < g.N && k < kend) {
+              if (g.wm == 0) v = g.W[(int64_t)n * g.ldw + k];
+              else v = g.W[((int64_t)(k / P) * g.ldw + n) * P + (k % P)];
+            }
+            rw[hh][i] = v;
+          }
+      }
     }
   };
   auto lstore = [&](int buf) {
-    if constexpr (BF) {
-      __bf16* As = reinterpret_cast<__bf16*>(lds[buf][0]);
-      __bf16* Ws = reinterpret_cast<__bf16*>(lds[buf][1]);
-      if (!g.at) {
-        const int r = t >> 2, kq = (t & 3) * 8;
-        bf16x8 v;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (__bf16)ra[i];
-        *reinterpret_cast<bf16x8*>(As + r * LDB + kq) = v;
+    for (int hh = 0; hh < HH; ++hh) {
+      const int ko = 32 * hh;
+      if constexpr (BF) {
+        __bf16* As = reinterpret_cast<__bf16*>(lds[buf][0]);
+        __bf16* Ws = reinterpret_cast<__bf16*>(lds[buf][1]);
+        if (!g.at) {
+          const int r = t >> 2, kq = (t & 3) * 8;
+          bf16x8 v;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = (__bf16)ra[hh][i];
+          *reinterpret_cast<bf16x8*>(As + r * TLDB + ko + kq) = v;
+        } else {
+          const int k = t >> 3, mq = (t & 7) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) As[(mq + i) * TLDB + ko + k] = (__bf16)ra[hh][i];
+        }
+        if (g.wm == 1) {
+          const int k = t >> 3, nq = (t & 7) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) Ws[(nq + i) * TLDB + ko + k] = (__bf16)rw[hh][i];
+        } else {
+          const int r = t >> 2, kq = (t & 3) * 8;
+          bf16x8 v;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = (__bf16)rw[hh][i];
+          *reinterpret_cast<bf16x8*>(Ws + r * TLDB + ko + kq) = v;
+        }
       } else {
-        const int k = t >> 3, mq = (t & 7) * 8;
+        float* As = lds[buf][0];
+        float* Ws = lds[buf][1];
+        if (!g.at) {
+          const int r = t >> 2, kq = (t & 3) * 8;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) As[(mq + i) * LDB + k] = (__bf16)ra[i];
+          for (int i = 0; i < 8; ++i) As[r * TLDK + ko + kq + i] = ra[hh][i];
+        } else {
+          const int k = t >> 3, mq = (t & 7) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) As[(mq + i) * TLDK + ko + k] = ra[hh][i];
+        }
+        if (g.wm == 1) {
+          const int k = t >> 3, nq = (t & 7) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) Ws[(nq + i) * TLDK + ko + k] = rw[hh][i];
+        } else {
+          const int r = t >> 2, kq = (t & 3) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) Ws[r * TLDK + ko + kq + i] = rw[hh][i];
+        }
       }
-      if (g.wm == 1) {
-        const int k = t >> 3, nq = (t & 7) * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Ws[(nq + i) * LDB + k] = (__bf16)rw[i];
-      } else {
-        const int r = t >> 2, kq = (t & 3) * 8;
-        bf16x8 v;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (__bf16)rw[i];
-        *reinterpret_cast<bf16x8*>(Ws + r * LDB + kq) = v;
-      }
-      return;
-    }
-    float* As = lds[buf][0];
-    float* Ws = lds[buf][1];
-    if (!g.at) {
-      const int r = t >> 2, kq = (t & 3) * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) As[r * LDK + kq + i] = ra[i];
-    } else {
-      const int k = t >> 3, mq = (t & 7) * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) As[(mq + i) * LDK + k] = ra[i];
-    }
-    if (g.wm == 1) {
-      const int k = t >> 3, nq = (t & 7) * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) Ws[(nq + i) * LDK + k] = rw[i];
-    } else {
-      const int r = t >> 2, kq = (t & 3) * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) Ws[r * LDK + kq + i] = rw[i];
     }
   };
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int nk = (kend - kbeg + TBK - 1) / TBK;
   gload(kbeg);
   lstore(0);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nk) gload(kbeg + (ks + 1) * BK);
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * TBK);
     if constexpr (BF) {
       const __bf16* As = reinterpret_cast<const __bf16*>(lds[buf][0]);
       const __bf16* Ws = reinterpret_cast<const __bf16*>(lds[buf][1]);
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (wmv * 32 + li) * LDB + 16 * kb + 8 * lh);
-        const bf16x8 w = *reinterpret_cast<const bf16x8*>(Ws + (wnv * 32 + li) * LDB + 16 * kb + 8 * lh);
+      for (int kb = 0; kb < TBK / 16; ++kb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (wmv * 32 + li) * TLDB + 16 * kb + 8 * lh);
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(Ws + (wnv * 32 + li) * TLDB + 16 * kb + 8 * lh);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w, acc, 0, 0, 0);
       }
     } else {
       const float* As = lds[buf][0];
       const float* Ws = lds[buf][1];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const float4 a = *reinterpret_cast<const float4*>(As + (wmv * 32 + li) * LDK + 16 * lh + 4 * s4);
-        const float4 w = *reinterpret_cast<const float4*>(Ws + (wnv * 32 + li) * LDK + 16 * lh + 4 * s4);
+      for (int s8 = 0; s8 < TBK / 8; ++s8) {  // lane half lh: k = (TBK / 2) lh + 4 s8 + j
+        const float4 a = *reinterpret_cast<const float4*>(As + (wmv * 32 + li) * TLDK + (TBK / 2) * lh + 4 * s8);
+        const float4 w = *reinterpret_cast<const float4*>(Ws + (wnv * 32 + li) * TLDK + (TBK / 2) * lh + 4 * s8);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a, j), f4c(w, j), acc, 0, 0, 0);
       }
@@ -274,7 +284,8 @@ static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_
   }
   int kper = K;
   if (splits > 1) {
-    kper = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+    const int ks = gc.bf16 ? TStep<true>::KS : TStep<false>::KS;
+    kper = ((K + splits - 1) / splits + ks - 1) / ks * ks;
     splits = (K + kper - 1) / kper;
   }
   TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, splits, kper,
