@@ -274,9 +274,12 @@ static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
   int splits = 1;
   const hipStream_t s = gc.s;
-  if (tiles < 128 && K >= 256 && gc.split) {
-    splits = (256 + tiles - 1) / tiles;
-    const int kmax = K / 128;
+  // few tiles: split to ~256 workgroups (>= 128 deep each); long K over < 512 tiles (the vocab-sized
+  // backward GEMMs, the weight gradients over all T*B rows): split to ~1024 (>= 512 deep each)
+  const bool small = tiles < 128 && K >= 256, deep = tiles < 512 && K >= 1024;
+  if ((small || deep) && gc.split) {
+    splits = small ? (256 + tiles - 1) / tiles : (1024 + tiles - 1) / tiles;
+    const int kmax = K / (small ? 128 : 512);
     if (splits > kmax) splits = kmax;
     const size_t capsp = gc.cap / ((size_t)M * N);
     if ((size_t)splits > capsp) splits = (int)capsp;
