@@ -912,11 +912,69 @@ __device__ __forceinline__ void lstm_gemm_partials(const bf16x8* af0, const bf16
   }
 }
 
+// Lean variant of lstm_gemm_partials (k_lstm<.., LEAN = true>): wave w owns ONE 32x32 block
+// (a = (w >> 1) & 1, c = w & 1) over one K half (w >> 2), a 2-chunk fragment ring, so the
+// workgroup needs ~half the VGPRs and one LDS tile instead of four: two workgroups fit on a CU
+// (one from each batch in flight) where the 8-partial version claims the whole CU.  Each fragment
+// is loaded by the two waves that share it (twice the L2 reads).  The K halves are summed as
+// (lower + upper) into the single tile Pt [column][row]; the caller reads it after a barrier.
+template <int H, class F>
+__device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
+                                               const bf16x8* wf1, float* Pt, F&& between) {
+  constexpr int KC = H / 16, CP = LS_CP, per = KC / 2, NR = 2;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
+  const bf16x8* af = a ? af1 : af0;
+  const bf16x8* wf = c ? wf1 : wf0;
+  const int kc0 = kh * per;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  bf16x8 fa[NR][3], fw[NR][3];
+  auto load = [&](int slot, int kc) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const size_t o = ((size_t)kc * 3 + q) * 64;
+      fa[slot][q] = af[o];
+      fw[slot][q] = wf[o];
+    }
+  };
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NR; ++i) load(i, kc0 + i);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  between();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < per; ++i) {
+    x3_step(acc, fa[i % NR], fw[i % NR]);
+    if (i + NR < per) load(i % NR, kc0 + i + NR);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;
+  if (kh) {
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4)
+      *reinterpret_cast<float4*>(dst + 8 * r4) = make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
+  }
+  __syncthreads();
+  if (!kh) {
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      float4* e = reinterpret_cast<float4*>(dst + 8 * r4);
+      const float4 v = *e;
+      *e = make_float4(acc[4 * r4] + v.x, acc[4 * r4 + 1] + v.y, acc[4 * r4 + 2] + v.z, acc[4 * r4 + 3] + v.w);
+    }
+  }
+}
+
 // G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
 // fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
 // gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
-template <int H, bool G = false>
-__global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+template <int H, bool G = false, bool LEAN = true>
+__global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
                                               const float* __restrict__ c_in, const int* __restrict__ par,
@@ -925,7 +983,7 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
                                               float* __restrict__ s_out, float* __restrict__ part) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
-  __shared__ __attribute__((aligned(16))) float lds[4 * TS + LS_TAIL_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[(LEAN ? 1 : 4) * TS + LS_TAIL_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
@@ -958,7 +1016,7 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
   // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
   float2 ta[4], xa[4], sa, sb, cprev;
   float4 wsv;
-  lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, [&] {
+  auto gathers = [&] {
     tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
     const int N5 = 5 * H;
     const float* trow = table + tk * N5;
@@ -974,19 +1032,24 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
     // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
     const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
     wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
-  });
-  __syncthreads();
+  };
+  if constexpr (LEAN) {
+    lstm_gemm_lean<H>(af0, af1, wf0, wf1, Pt, gathers);
+  } else {
+    lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, gathers);
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
-    const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
-    const float* sp = Pt + cq * CP + r4;
-    float4 v[4];
+    for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
+      const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
+      const float* sp = Pt + cq * CP + r4;
+      float4 v[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
-    float4 o;
+      for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
+      float4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
-    *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
+      for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
+      *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
+    }
   }
   __syncthreads();
   float gate[4][2];
@@ -997,18 +1060,18 @@ __global__ __launch_bounds__(512) void k_lstm(int B, int V, const int64_t* __res
 #pragma unroll
       for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
   }
-  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + 4 * TS, h_out, hsp_out, c_out, s_out, part);
+  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + (LEAN ? 1 : 4) * TS, h_out, hsp_out, c_out, s_out, part);
 }
 
-// Split LSTM step, part 1: G = h_{t-1} W_hh^T (the tile sums of k_lstm, same fixed order) written
+// Split LSTM step, part 1: G = h_{t-1} W_hh^T (the tile of k_lstm, same lean partials and order) written
 // to gates [B][H/16 tiles][8 unit pairs][4 gates][2 units] -- the order k_lstm_cell's threads read
 // (two float4 each).  Depends only on h_{t-1}, so the decode loop runs it on a second stream beside
 // the previous step's attention, vocab screen and rescoring (the token is not needed here).
 template <int H>
-__global__ __launch_bounds__(512) void k_lstm_gemm(int B, const bf16x8* __restrict__ hsp_in,
+__global__ __launch_bounds__(512, 4) void k_lstm_gemm(int B, const bf16x8* __restrict__ hsp_in,
                                                    const bf16x8* __restrict__ whh3, float* __restrict__ gates) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP, NTn = H / 16, KC = H / 16;
-  __shared__ __attribute__((aligned(16))) float Pt[4 * TS];
+  __shared__ __attribute__((aligned(16))) float Pt[TS];
   const int MT = (B + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
   const int nt = L / MT, mt = L % MT;
@@ -1018,7 +1081,7 @@ __global__ __launch_bounds__(512) void k_lstm_gemm(int B, const bf16x8* __restri
   const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
   const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
   const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
-  lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, [] {});
+  lstm_gemm_lean<H>(af0, af1, wf0, wf1, Pt, [] {});
   __syncthreads();
   const int rr = t >> 3, pp = t & 7, m = m0 + rr;
   float o[8];
@@ -1027,7 +1090,7 @@ __global__ __launch_bounds__(512) void k_lstm_gemm(int B, const bf16x8* __restri
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const float* sp = Pt + (16 * g + 2 * pp + q) * CP + rr;
-      o[2 * g + q] = (sp[0] + sp[TS]) + (sp[2 * TS] + sp[3 * TS]);
+      o[2 * g + q] = sp[0];
     }
   if (m < B) {
     float4* dst = reinterpret_cast<float4*>(gates + (((int64_t)m * NTn + nt) * 8 + pp) * 8);
