@@ -14,7 +14,9 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int
 
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libadaptive_amd.so")
+# AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
+LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                         "libadaptive_amd.so")
 ABI_VERSION = 10
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2

@@ -1634,8 +1634,8 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const 
 //   fragments of the 5 column blocks are shared by the 4 waves through LDS, staged in SC2_KS-chunk
 //   stages (register prefetch of stage s+1 under the MFMAs of stage s, two LDS buffers, one
 //   barrier per stage).  The epilogue is the 64 x 64 form's, per 32 x 32 block.
-constexpr int SC2_BM = 128, SC2_NB = 5, SC2_BN = 32 * SC2_NB, SC2_KS = 8;
-constexpr int SC2_STAGE = SC2_NB * SC2_KS * 64;  // bf16x8 per LDS stage (40 KB)
+constexpr int SC2_BM = 128, SC2_NB = 5, SC2_BN = 32 * SC2_NB, SC2_KS = 4;
+constexpr int SC2_STAGE = SC2_NB * SC2_KS * 64;  // bf16x8 per LDS stage (20 KB)
 
 // Per (row, granule) summary of one 32 x 32 block of screened logits in MFMA C layout (rows row0..,
 // columns 32 G..): keys, transposing top-2 butterfly, bound E, one float4 per row (see k_vscreen).
@@ -1675,7 +1675,7 @@ __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0,
 }
 
 template <int H>
-__global__ __launch_bounds__(256) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+__global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
                                                   const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
                                                   const float2* __restrict__ gs, const float* __restrict__ bias,
                                                   float4* __restrict__ summ) {
@@ -1687,13 +1687,16 @@ __global__ __launch_bounds__(256) void k_vscreen2(int B, int V, int Vp, const bf
   const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31;
   const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
-  // this wave's u fragments: row block (m0 / 32 + wave), every k16 chunk -- one round trip
-  bf16x8 fa[KC];
-  {
-    const bf16x8* a0 = ua + (size_t)((m0 >> 5) + wave) * KC * 64 + lane;
+  // this wave's u fragments (row block m0 / 32 + wave) arrive one stage ahead, like the W stage:
+  // a two-stage register ring instead of all KC chunks at once, so the kernel fits in 256 registers
+  // (two waves per SIMD) and 40 KB of LDS -- two workgroups per CU, one per batch in flight
+  const bf16x8* a0 = ua + (size_t)((m0 >> 5) + wave) * KC * 64 + lane;
+  bf16x8 fa[2][SC2_KS];
+  auto uload = [&](int s, int slot) {
 #pragma unroll
-    for (int c = 0; c < KC; ++c) fa[c] = a0[(size_t)c * 64];
-  }
+    for (int c = 0; c < SC2_KS; ++c) fa[slot][c] = a0[(size_t)(s * SC2_KS + c) * 64];
+  };
+  uload(0, 0);
   // W stage s: for column block b (0..4), chunks [s KS, (s+1) KS) are one contiguous 8 KB run of the
   // fragment-order W_m; thread t moves bf16x8 j = t + 256 i of the stage (b = j / (KS*64)).
   const bf16x8* wbase = wf + (size_t)(n0 >> 5) * KC * 64;
@@ -1725,7 +1728,10 @@ __global__ __launch_bounds__(256) void k_vscreen2(int B, int V, int Vp, const bf
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     lstore(s & 1);
-    if (s + 1 < NS) gload(s + 1);
+    if (s + 1 < NS) {
+      gload(s + 1);
+      uload(s + 1, (s + 1) & 1);
+    }
     __syncthreads();
     const bf16x8* ws = Ws[s & 1] + lane;
 #pragma unroll
@@ -1733,7 +1739,7 @@ __global__ __launch_bounds__(256) void k_vscreen2(int B, int V, int Vp, const bf
 #pragma unroll
       for (int b = 0; b < SC2_NB; ++b) {
         const bf16x8 w = ws[(b * SC2_KS + c) * 64];
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s * SC2_KS + c], w, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][c], w, acc[b], 0, 0, 0);
       }
     }
   }
