@@ -7,8 +7,9 @@ Mirrors the reference module tree and public surface so callers (``code_src/tool
 * ``Encoder2Decoder(cf)``             — adaptive_attention.py:159-165
 * ``.sampler(images, max_len=30)``   — adaptive_attention.py:168-216  -> (ids, alpha, beta)
 * ``.encoder(images)``                — AttentiveCNN.forward, baseline_attention.py:36-62
-* ``.decoder(V, v_g, captions, states)`` with one-token captions — Decoder.forward,
-  baseline_attention.py:148-194 (-> scores, alpha, beta, states)
+* ``.decoder(V, v_g, captions, states)`` — Decoder.forward, baseline_attention.py:148-194
+  (-> scores, alpha, beta, states): one-token captions run the sampling step, whole captions [B,T]
+  the teacher-forced recurrence
 * state-dict keys identical to the reference (``encoder.affine_a.weight``, ``decoder.LSTM.*``,
   ``decoder.adaptive.{sentinel,atten,mlp}.*``).
 
@@ -231,6 +232,9 @@ class Encoder2Decoder(nn.Module):
         # True: teacher-forced training (forward()) with every GEMM on bf16 MFMA (bf16 operands, fp32
         # accumulation: BASELINE config 5); False: fp32 GEMMs
         self.train_bf16 = False
+        # True: sampler() shards the batch over the ranks of the default torch.distributed group
+        # (one process per GPU) and all-gathers the results (sharded_sampler); opt-in
+        self.distributed_sampler = False
         self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
         self._plan_seen = set()
 
@@ -339,7 +343,18 @@ class Encoder2Decoder(nn.Module):
         ``lanes`` (default ``self.decode_lanes``) splits the step loop over that many HIP streams by
         row blocks so the lanes' kernels overlap; captions are independent, results are identical.
         ``graph`` (default ``self.decode_graph``): repeated calls on the same input buffer replay a
-        captured hipGraph of the whole decode (C-ABI aa_decode_plan); results are identical."""
+        captured hipGraph of the whole decode (C-ABI aa_decode_plan); results are identical.
+        With ``self.distributed_sampler = True`` and an initialised multi-rank process group, every
+        rank passes the whole batch and the call runs ``sharded_sampler`` (the reference's sampler
+        distributes itself over the visible GPUs, adaptive_attention.py:178-181)."""
+        if self.distributed_sampler and trace is None:
+            import torch.distributed as dist
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                return self.sharded_sampler(images, max_len)
+        return self._sampler_local(images, max_len, trace, exact_vocab, lanes, graph)
+
+    @torch.no_grad()
+    def _sampler_local(self, images, max_len, trace=None, exact_vocab=False, lanes=None, graph=None):
         images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
@@ -389,6 +404,29 @@ class Encoder2Decoder(nn.Module):
         return ids, alpha, beta
 
     @torch.no_grad()
+    def sharded_sampler(self, images: torch.Tensor, max_len: int = 30, total: Optional[int] = None, group=None,
+                        gather_attention: bool = True):
+        """Multi-rank ``sampler``: the one-process-per-GPU counterpart of the reference's
+        self-distributing sampler (``nn.DataParallel`` over every visible GPU,
+        adaptive_attention.py:178-181).  Every rank of ``group`` (``torch.distributed``; ``nccl`` =
+        RCCL on ROCm) calls it; rank r decodes the contiguous row block ``shard_bounds(total,
+        world, r)`` and one all-gather of the ids (and, with ``gather_attention``, alpha / beta)
+        returns the whole batch's results on every rank -- the same values as one ``sampler`` call
+        over all rows (rows never interact, and no kernel's per-row arithmetic depends on the batch
+        size).  ``images``: the full batch on every rank (``total=None``), or this rank's block of a
+        ``total``-row batch."""
+        import torch.distributed as dist
+        from . import distributed as D
+        if not dist.is_initialized():
+            raise RuntimeError("sharded_sampler needs an initialised torch.distributed process group")
+        if total is None:
+            total = images.size(0)
+            images = D.local_rows(images, group)
+        ids, alpha, beta = D.sharded_sampler(lambda x, t: self._sampler_local(x, t), images, int(total), int(max_len),
+                                             group=group, gather_attention=gather_attention)
+        return ids, alpha, beta
+
+    @torch.no_grad()
     def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2,
                     exact_vocab: bool = False):
         """Beam-search decode (BASELINE config 4; not in the reference, semantics in
@@ -433,6 +471,10 @@ class Encoder2Decoder(nn.Module):
     def _train_flags(self) -> int:
         return _lib.TRAIN_BF16 if getattr(self, "train_bf16", False) else 0
 
+    def _decode_flags(self) -> int:
+        """Flags of a default greedy decode (what sampler passes without exact_vocab)."""
+        return (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0) | self._lstm_flags()
+
     def _lstm_flags(self) -> int:
         return ((0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
                 | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0))
@@ -476,17 +518,22 @@ class Encoder2Decoder(nn.Module):
         _lib.check(rc, "encoder_tail")
         return V, v_g, (h0, c0), a_g, VWv
 
-    # ---- Decoder.forward with one-token captions (baseline_attention.py:148-194) -----------------
+    # ---- Decoder.forward (baseline_attention.py:148-194) ------------------------------------------
     @torch.no_grad()
     def _decode_step(self, V, v_g, captions, states):
+        """One-token captions [B,1]: the sampling step (aa_decode_step, sentinel h_{t-1} = 0).
+        Whole captions [B,T], T > 1: the teacher-forced recurrence over T steps (aa_decoder_forward,
+        the forward kernels of the training path) -> scores [B,T,V], alpha [B,T,49], beta [B,T,1],
+        (h, c) [1,B,H] after the last step.  No autograd graph here: gradients flow through
+        ``Encoder2Decoder.forward`` (aa_train_forward / aa_train_backward)."""
         d = self.dims
-        if captions.dim() != 2 or captions.size(1) != 1:
-            raise NotImplementedError(
-                "adaptive_amd: Decoder.forward is implemented for one-token steps (sampling). Teacher-forced "
-                "multi-step decoding (training, SURVEY.md §8f row 1) is not built yet.")
+        if captions.dim() != 2:
+            raise ValueError(f"captions must be [B, T] token ids, got {tuple(captions.shape)}")
         B, dev = V.size(0), V.device
         if states is None:
             raise ValueError("states (h, c) are required")
+        if captions.size(1) != 1:
+            return self._decode_steps(V, v_g, captions, states)
         h, c = states
         # accept [1,B,H] (LSTM layout) or [B,1,H] (encoder output layout)
         h = h.reshape(B, d.hidden).contiguous()
@@ -512,6 +559,39 @@ class Encoder2Decoder(nn.Module):
                                     ws.numel() if ws is not None else 0, _lib.stream_handle())
         _lib.check(rc, "decode_step")
         self._last_tokens = tok_out
+        return scores, alpha, beta, (h_out, c_out)
+
+    def _decode_steps(self, V, v_g, captions, states):
+        d = self.dims
+        B, T, dev = V.size(0), captions.size(1), V.device
+        if captions.size(0) != B or tuple(V.shape[1:]) != (ATT, d.hidden) or tuple(v_g.shape) != (B, d.embed):
+            raise ValueError("decoder: V [B,49,H], v_g [B,E] and captions [B,T] must agree")
+        h, c = states
+        h = h.reshape(B, d.hidden).float().contiguous()
+        c = c.reshape(B, d.hidden).float().contiguous()
+        caps = captions.to(device=dev, dtype=torch.int64).contiguous()
+        if B and (int(caps.min()) < 0 or int(caps.max()) >= d.vocab):
+            raise IndexError("index out of range in self (embedding)")  # nn.Embedding's error
+        for x in (V, v_g, h, c):
+            if not x.is_cuda:
+                raise RuntimeError("adaptive_amd: decoder inputs must be CUDA (ROCm) tensors")
+        lib = _lib.load()
+        params = dict(self.named_parameters())
+        w = _lib.RefWeights(**{f: params[k].data_ptr() for f, k in _lib.WEIGHT_FIELDS})
+        V, v_g = V.float().contiguous(), v_g.float().contiguous()
+        scores = torch.empty(B, T, d.vocab, device=dev)
+        alpha = torch.empty(B, T, ATT, device=dev)
+        beta = torch.empty(B, T, 1, device=dev)
+        h_out = torch.empty(1, B, d.hidden, device=dev)
+        c_out = torch.empty(1, B, d.hidden, device=dev)
+        nbytes = lib.aa_decoder_workspace_bytes(self._c_dims(), B, T)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.aa_decoder_forward(w, self._c_dims(), V.data_ptr(), v_g.data_ptr(), h.data_ptr(), c.data_ptr(), B,
+                                        T, caps.data_ptr(), caps.stride(0), scores.data_ptr(), alpha.data_ptr(),
+                                        beta.data_ptr(), h_out.data_ptr(), c_out.data_ptr(), ws.data_ptr(), nbytes,
+                                        self._train_flags(), _lib.stream_handle())
+        _lib.check(rc, "decoder_forward")
         return scores, alpha, beta, (h_out, c_out)
 
     # ---- AdaptiveBlock.mlp on given rows (adaptive_attention.py:132) ----------------------------

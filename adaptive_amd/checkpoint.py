@@ -4,14 +4,21 @@ The reference saves ``model.state_dict()`` with ``torch.save`` after every epoch
 ``cider-%.4f_model-%d.pkl`` (``code_src/train.py:177-178``) and restores it with
 ``model.load_state_dict(torch.load(path))`` (``code_src/models/model_factory.py:15-16``,
 ``code_src/tools/utils.py:263-266``).  ``Encoder2Decoder`` here has the same state-dict keys and
-shapes, so the files are interchangeable; loading always uses ``torch.load(weights_only=True)``
-(tensors only, nothing executed from the file).  A reference checkpoint's ResNet trunk keys
-(``encoder.resnet_conv.*``) are dropped by ``Encoder2Decoder.load_state_dict`` (the trunk is not
-part of this path).
+shapes; loading always uses ``torch.load(weights_only=True)`` (tensors only, nothing executed from
+the file).  A reference checkpoint's ResNet trunk keys (``encoder.resnet_conv.*``) are dropped by
+``Encoder2Decoder.load_state_dict`` when the model runs on post-trunk features.
+
+Direction matters for the trunk: the reference's module always has the trunk and loads strictly
+(``model.load_state_dict(torch.load(...))``), so a file written from a trunk-less model (the
+default ``Encoder2Decoder(cf)``) lacks the 930 ``encoder.resnet_conv.*`` tensors and loads there
+only with ``strict=False``.  Models built with ``trunk=True`` (or ``save_checkpoint(...,
+trunk_state=...)`` with a torchvision-layout trunk state dict) write complete files that the
+reference loads strictly.
 """
 from __future__ import annotations
 
 import os
+from typing import Dict, Optional
 
 import torch
 
@@ -21,11 +28,20 @@ def checkpoint_name(cider: float, epoch: int) -> str:
     return "cider-%.4f_model-%d.pkl" % (cider, epoch)
 
 
-def save_checkpoint(model: torch.nn.Module, directory: str, cider: float, epoch: int) -> str:
+def save_checkpoint(model: torch.nn.Module, directory: str, cider: float, epoch: int,
+                    trunk_state: Optional[Dict[str, torch.Tensor]] = None) -> str:
     """``train.py:177-178``: the state dict (all tensors moved to the CPU so the file loads on
-    any host) under the reference's epoch file name; returns the path."""
+    any host) under the reference's epoch file name; returns the path.  ``trunk_state``: the
+    ResNet-152 trunk's state dict (torchvision child layout, ``adaptive_amd.trunk.resnet_conv``)
+    written under ``encoder.resnet_conv.*`` when the model has no trunk of its own, so that the
+    reference's strict ``load_state_dict`` accepts the file (module docstring)."""
     path = os.path.join(directory, checkpoint_name(cider, epoch))
-    torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()}, path)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    if trunk_state is not None:
+        if any(k.startswith("encoder.resnet_conv.") for k in sd):
+            raise ValueError("the model already carries a trunk; trunk_state would overwrite it")
+        sd.update({"encoder.resnet_conv." + k: v.detach().cpu() for k, v in trunk_state.items()})
+    torch.save(sd, path)
     return path
 
 

@@ -840,6 +840,40 @@ size_t aa_train_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 
 static inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
 
+// Decoder.forward over T teacher-forced steps (baseline_attention.py:148-194 with the adaptive
+// block, adaptive_attention.py:110-134) from V, v_g, (h0, c0) already in the workspace: every
+// activation of the T steps (Hs, Cs, S, alpha, beta, U = c_hat + h, ...) lands in ws, t-major.
+static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const TrainWS& s, const aa_dims& d, int B,
+                         int T, const int64_t* tokens, int tok_ld) {
+  using namespace aa;
+  const int H = d.hidden, E = d.embed, V = d.vocab, R = T * B;
+  const hipStream_t st = gc.s;
+  tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
+  // x_t and the step-invariant input terms for all steps
+  hipLaunchKernelGGL(k_tr_x, dim3(R), dim3(256), 0, st, tokens, tok_ld, w->embed_w, V, E, s.vg, B, T, s.X);
+  tgemm(gc, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
+  tgemm(gc, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
+  // LSTM over T steps (baseline_attention.py:167-178)
+  for (int t = 0; t < T; ++t) {
+    const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
+    const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
+    tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
+    hipLaunchKernelGGL(k_tr_cell, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.G4, s.PRE + (size_t)t * B * 5 * H,
+                       5 * H, cp, B, H, s.Hs + (size_t)t * B * H, s.Cs + (size_t)t * B * H,
+                       s.GA + (size_t)t * B * 4 * H);
+  }
+  // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
+  hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
+                     (int64_t)H, R, H);
+  tgemm(gc, R - B, H, H, s.Hs, H, 0, w->sent_affine_h_w, H, 0, s.SG + (size_t)B * H, H, 1);
+  hipLaunchKernelGGL(k_tr_sent, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.SG, s.Cs, s.S, (int64_t)R * H);
+  // attention projections and the attention itself (adaptive_attention.py:26-58)
+  tgemm(gc, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
+  tgemm(gc, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
+  hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs, s.S,
+                     s.alpha, s.beta, s.ctx, s.U);
+}
+
 int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
                      const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, float* scores, int32_t N,
                      void* workspace, size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
@@ -865,33 +899,73 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   tgemm(gc, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
-  tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
-  // x_t and the step-invariant input terms for all steps
-  hipLaunchKernelGGL(k_tr_x, dim3(R), dim3(256), 0, st, tokens, tok_ld, w->embed_w, V, E, s.vg, B, T, s.X);
-  tgemm(gc, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
-  tgemm(gc, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
-  // LSTM over T steps (baseline_attention.py:167-178)
-  for (int t = 0; t < T; ++t) {
-    const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
-    const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
-    tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
-    hipLaunchKernelGGL(k_tr_cell, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.G4, s.PRE + (size_t)t * B * 5 * H,
-                       5 * H, cp, B, H, s.Hs + (size_t)t * B * H, s.Cs + (size_t)t * B * H,
-                       s.GA + (size_t)t * B * 4 * H);
-  }
-  // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
-  hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
-                     (int64_t)H, R, H);
-  tgemm(gc, R - B, H, H, s.Hs, H, 0, w->sent_affine_h_w, H, 0, s.SG + (size_t)B * H, H, 1);
-  hipLaunchKernelGGL(k_tr_sent, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.SG, s.Cs, s.S, (int64_t)R * H);
-  // attention projections and the attention itself (adaptive_attention.py:26-58)
-  tgemm(gc, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
-  tgemm(gc, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
-  hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs, s.S,
-                     s.alpha, s.beta, s.ctx, s.U);
+  decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
   // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
   hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
   tgemm(gc, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
+  return aa_launch_status();
+}
+
+// batch-first row of t-major row r = t B + b: b T + t (Decoder.forward returns [B, T, ...])
+__global__ void k_bt_rowmap(int B, int T, int* __restrict__ map) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B * T) map[r] = (r % B) * T + r / B;
+}
+
+// alpha [R][PP], beta [R] (t-major) -> alpha_out [B][T][P], beta_out [B][T]
+__global__ void k_bt_atten_out(int B, int T, const float* __restrict__ alpha, const float* __restrict__ beta,
+                               float* __restrict__ alpha_out, float* __restrict__ beta_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b, t, k) over k < P + 1
+  if (i >= (int64_t)B * T * (aa::P + 1)) return;
+  const int k = (int)(i % (aa::P + 1));
+  const int bt = (int)(i / (aa::P + 1)), b = bt / T, t = bt % T;
+  const int64_t r = (int64_t)t * B + b;
+  if (k < aa::P) {
+    if (alpha_out) alpha_out[(int64_t)bt * aa::P + k] = alpha[r * aa::PP + k];
+  } else if (beta_out) {
+    beta_out[bt] = beta[r];
+  }
+}
+
+size_t aa_decoder_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
+  return aa_train_workspace_bytes(d, B, T);
+}
+
+int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, const float* V, const float* v_g,
+                       const float* h0, const float* c0, int32_t B, int32_t T, const int64_t* tokens, int32_t tok_ld,
+                       float* scores, float* alpha, float* beta, float* h_out, float* c_out, void* workspace,
+                       size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
+  using namespace aa;
+  int rc = train_check(dims, B, T);
+  if (rc) return rc;
+  if (B == 0 || T == 0) return AA_OK;
+  if (!w || !V || !v_g || !h0 || !c0 || !tokens || !workspace || !w->sent_affine_h_w) return AA_ERR_NULL;
+  if (tok_ld < T) return AA_ERR_SHAPE;
+  size_t need;
+  TrainWS s = carve_train(static_cast<char*>(workspace), *dims, B, T, B * T, &need);
+  if (workspace_bytes < need) return AA_ERR_BUFFER;
+  const int H = dims->hidden, E = dims->embed, Vc = dims->vocab, R = T * B;
+  hipStream_t st = (hipStream_t)stream;
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
+  hipError_t e = hipSuccess;
+  if (!e) e = hipMemcpyAsync(s.V, V, sizeof(float) * (size_t)B * P * H, hipMemcpyDeviceToDevice, st);
+  if (!e) e = hipMemcpyAsync(s.vg, v_g, sizeof(float) * (size_t)B * E, hipMemcpyDeviceToDevice, st);
+  if (!e) e = hipMemcpyAsync(s.h0, h0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
+  if (!e) e = hipMemcpyAsync(s.c0, c0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
+  if (e) return (int)e;
+  decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
+  if (scores) {  // mlp(c_hat + h) for every (b, t), batch-first (:132)
+    hipLaunchKernelGGL(k_bt_rowmap, dim3(nblk(R)), dim3(256), 0, st, B, T, s.prow);
+    tgemm(gc, R, Vc, H, s.U, H, 0, w->mlp_w, H, 0, scores, Vc, 0, w->mlp_b, nullptr, 0, nullptr, s.prow);
+  }
+  if (alpha || beta)
+    hipLaunchKernelGGL(k_bt_atten_out, dim3(nblk((int64_t)R * (P + 1))), dim3(256), 0, st, B, T, s.alpha, s.beta,
+                       alpha, beta);
+  if (h_out) e = hipMemcpyAsync(h_out, s.Hs + (size_t)(T - 1) * B * H, sizeof(float) * (size_t)B * H,
+                                hipMemcpyDeviceToDevice, st);
+  if (!e && c_out) e = hipMemcpyAsync(c_out, s.Cs + (size_t)(T - 1) * B * H, sizeof(float) * (size_t)B * H,
+                                      hipMemcpyDeviceToDevice, st);
+  if (e) return (int)e;
   return aa_launch_status();
 }
 

@@ -28,6 +28,10 @@ def shard_bounds(total: int, world: int, rank: int) -> Tuple[int, int]:
 def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
     if dist.get_backend(group) == "nccl":  # RCCL: one fused all-gather into the output buffer
         dist.all_gather_into_tensor(out, inp, group=group)
+    elif out.is_cuda:  # gloo over device tensors (multi-process tests on one GPU): stage through the host
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather(list(host.chunk(dist.get_world_size(group))), inp.cpu(), group=group)
+        out.copy_(host)
     else:  # gloo (CPU tests)
         dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
 
@@ -51,10 +55,21 @@ def gather_rows(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
     return torch.cat([buf[r * width: r * width + counts[r]] for r in range(world)], dim=0)
 
 
+def local_rows(images: torch.Tensor, group=None) -> torch.Tensor:
+    """This rank's contiguous row block of a batch every rank holds in full."""
+    lo, hi = shard_bounds(images.size(0), dist.get_world_size(group), dist.get_rank(group))
+    return images[lo:hi]
+
+
 def sharded_sampler(decode: Callable[[torch.Tensor, int], Tuple[torch.Tensor, ...]], images_local: torch.Tensor,
                     total: int, max_len: int, group=None, gather_attention: bool = False):
     """Decode this rank's rows with ``decode(images, max_len) -> (ids, alpha, beta)`` and all-gather
-    the ids (and optionally alpha/beta) to every rank."""
+    the ids (and optionally alpha/beta) to every rank.  ``images_local`` is the rank's
+    ``shard_bounds(total, world, rank)`` block of the ``total``-row batch."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_bounds(total, world, rank)
+    if images_local.size(0) != hi - lo:
+        raise ValueError(f"rank {rank} was given {images_local.size(0)} rows, its shard of {total} is {hi - lo}")
     ids, alpha, beta = decode(images_local, max_len)
     ids_all = gather_rows(ids, total, group)
     if not gather_attention:

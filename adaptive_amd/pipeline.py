@@ -71,12 +71,13 @@ class DecodePipeline:
         s.wait_event(ready)
         slot.aux.wait_event(ready)
         images.record_stream(s)
+        flags = m._decode_flags()  # the same flags sampler() passes (fp32_encoder included)
         with torch.cuda.device(dev), torch.cuda.stream(s):
-            key = (images.data_ptr(), B, T, m._packed.data_ptr(), m._lstm_flags())
+            key = (images.data_ptr(), B, T, m._packed.data_ptr(), flags)
             plan = slot.plans.get(key) if self.graph else None
             if plan is None and self.graph and key in slot.seen and B > 0 and T > 0:
                 s.synchronize()
-                plan = slot.plans[key] = _Plan(lib, model, images, B, T, m._lstm_flags(), 1, m._c_dims(), dev)
+                plan = slot.plans[key] = _Plan(lib, model, images, B, T, flags, 1, m._c_dims(), dev)
                 while len(slot.plans) > self.MAX_PLANS:
                     slot.plans.popitem(last=False)
             slot.seen.add(key)
@@ -92,7 +93,7 @@ class DecodePipeline:
                     slot.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
                                               beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None,
-                                              m._lstm_flags(), s.cuda_stream,
+                                              flags, s.cuda_stream,
                                               # the other slots already fill the chip: one stream per slot
                                               # unless the LSTM steps are split
                                               slot.aux.cuda_stream if m.split_lstm else None)

@@ -6,19 +6,21 @@
 
 A "step" = one sampler() call over this rank's B = 512 synthetic images (post-trunk features
 [B,2048,7,7], U[0,1), counter-based; random-init weights of the reference architecture, seed 123)
-plus, for N > 1, the RCCL all-gather of the token ids (the path's only collective).  Each rank
+plus, for N > 1, the RCCL all-gather of the token ids (the path's only collective,
+adaptive_amd.distributed.gather_rows), plus the ids device -> host copy.  Each rank
 decodes its own rows (weak scaling: global batch = 512 N).  Inputs are resident in HBM before the
-timed region.  Rank 0 prints ONE JSON line.
+timed region, one distinct feature batch per batch in flight.  Every mode is timed over >= 5
+regions of exactly K steps and the median region is reported.  Rank 0 prints ONE JSON line.
 
 Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic FLOPs / its average
-HIP-event duration inside the timed region), ``kernels`` (all per-kernel averages),
-``path_roofline`` (whole decode vs the fp32 MFMA peak), ``cpu_baseline`` (the PyTorch-CPU
-restatement of the reference sampler, oracle/adaptive_oracle.py, timed on this host, rank 0, N=1).
+HIP-event duration inside a traced region), ``kernels`` (all per-kernel averages),
+``path_roofline`` (every kernel's executed work at its own ceiling, summed, over the measured time
+per batch), ``cpu_baseline`` (the PyTorch-CPU restatement of the reference sampler,
+oracle/adaptive_oracle.py, timed on this host's cores, rank 0, N=1).
 """
 from __future__ import annotations
 
 import argparse
-import itertools
 import json
 import os
 import sys
@@ -35,6 +37,7 @@ from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
 from adaptive_amd import _lib  # noqa: E402
 from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
 from adaptive_amd.hip_events import EventArray  # noqa: E402
+from adaptive_amd.distributed import gather_rows  # noqa: E402
 from adaptive_amd.pipeline import DecodePipeline  # noqa: E402
 
 METRIC = "captions/sec (greedy, max_len=20) at B=512; 1/2/4/8-GPU scaling"
@@ -101,11 +104,8 @@ def atten_bytes_per_row() -> int:
     return 4 * (P * H + P * P + (H // 16) * 2 * P + 2 * H + H + P + 1) + 2 * H
 
 
-def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
-    from oracle.adaptive_oracle import OracleModel  # test/baseline infrastructure only
-    threads = int(os.environ.get("AA_CPU_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+def _time_cpu_sampler(m, feats_cpu, T, threads, budget_s):
     torch.set_num_threads(threads)
-    m = OracleModel(synth.make_weights(123))
     m.sampler(feats_cpu[:8], max_len=2)  # warm-up
     times = []
     t_end = time.perf_counter() + budget_s
@@ -113,6 +113,46 @@ def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
         t0 = time.perf_counter()
         m.sampler(feats_cpu, max_len=T)
         times.append(time.perf_counter() - t0)
+    return times
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def available_cpus() -> dict:
+    """CPUs this process may actually use: its affinity set, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max / v1 cfs quota).  On the GPU box the affinity lists the whole machine (256)
+    while the job's quota is 16 CPUs; torch at 64 threads there runs the oracle 3.5x slower than at
+    16 (profiles/r02_cpu_threads_probe.log)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                quota = -(-int(parts[0]) // int(parts[1]))
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
+                    quota = -(-int(parts[0]) // int(g.read()))
+            if quota:
+                break
+        except (OSError, ValueError, IndexError):
+            continue
+    return {"affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota) if quota else aff}
+
+
+def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
+    """The oracle's PyTorch-CPU sampler (oracle/adaptive_oracle.py, reference op order) on this
+    host with one thread per CPU the process may use (SURVEY.md §8d's len(sched_getaffinity(0)),
+    capped by the cgroup quota: available_cpus).  Median of up to 5 whole-batch runs."""
+    from oracle.adaptive_oracle import OracleModel  # test/baseline infrastructure only
+    cpus = available_cpus()
+    threads = int(os.environ.get("AA_CPU_THREADS", "0")) or cpus["usable"]
+    m = OracleModel(synth.make_weights(123))
+    times = _time_cpu_sampler(m, feats_cpu, T, threads, budget_s)
     med = float(np.median(times))
     cpu_model = ""
     try:
@@ -124,7 +164,28 @@ def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
     return {"value": B / med, "unit": "captions/s", "cores": threads, "kind": "port",
             "sample": f"oracle/adaptive_oracle.py sampler (PyTorch-CPU fp32 restatement of the reference, "
                       f"reference op order) on the same B={B}, max_len={T} batch; median of {len(times)} runs "
-                      f"({', '.join(f'{t:.2f}' for t in times)} s); {threads} threads; {cpu_model}"}
+                      f"({', '.join(f'{t:.2f}' for t in times)} s) at {threads} threads = every CPU this process may "
+                      f"use (affinity {cpus['affinity']} CPUs, cgroup quota {cpus['cgroup_quota']} CPUs); {cpu_model}",
+            "cpus": cpus}
+
+
+def path_ideal_seconds(B: int, T: int, Vp: int = 10240) -> dict:
+    """Executed work of one decode priced at each kernel's own ceiling: bf16x3 GEMMs
+    at bf16 peak / 6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen (all Vp padded
+    columns) at the bf16 peak, the attention and rescoring at HBM peak for their bytes.  The sum is
+    the time a decode would take if every kernel ran at its roofline, back to back."""
+    f = flops_per_caption(T)
+    parts = {
+        "k_enc_v4": f["k_enc_v"] * B / PEAK_X3,
+        "k_enc_heads3": f["k_enc_heads"] * B / PEAK_X3,
+        "k_gemm_bias(VWv)": f["vwv"] * B / PEAK_FP32,
+        "k_gemm_bias(x_g)": f["xg"] * B / PEAK_FP32,
+        "k_lstm": T * (f["k_lstm_gemm"] * B / PEAK_X3 + f["proj"] * B / PEAK_FP32),
+        "k_atten": T * atten_bytes_per_row() * B / PEAK_HBM,
+        "k_vscreen": T * 2 * H * Vp * B / PEAK_BF16,
+        "k_vrescore": T * kernel_costs(B, T)["k_vrescore"][1] / PEAK_HBM,
+    }
+    return {"total": sum(parts.values()), "parts": parts}
 
 
 def main():
@@ -150,6 +211,7 @@ def main():
                     "128x160 (k_vscreen2)")
     ap.add_argument("--enc-v3", action="store_true", help="encoder V GEMM on k_enc_v3 (128x128 tiles) instead of "
                     "k_enc_v4 (two images per workgroup, all columns)")
+    ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -170,26 +232,37 @@ def main():
     model.screen64 = args.screen64
     model.enc_v3 = args.enc_v3
     enc_name = "k_enc_v3" if args.enc_v3 else "k_enc_v4"
-    feats = synthetic_features(B, dev, seed=0, row0=rank * B)  # rows [rank*B, (rank+1)*B) of the global batch
-    ids_all = torch.empty(world * B, T, dtype=torch.int64, device=dev) if world > 1 else None
-
-    def step(trace=None):
-        ids, alpha, beta = model.sampler(feats, max_len=T, trace=trace, lanes=args.lanes, graph=not args.no_graph)
-        if world > 1:
-            dist.all_gather_into_tensor(ids_all, ids)
-        return ids
-
     depth = max(1, args.pipeline_depth)
+    # distinct resident feature batches: each batch in flight reads its own 205 MB
+    # map, so nothing is served from the 256 MB MALL left behind by the previous batch.  Buffer 0 is
+    # the canonical batch (rows [rank B, (rank+1) B) of the seed-0 global batch); the others use
+    # seeds 1.. for the same rows.
+    nbuf = max(depth, 2)
+    bufs = [synthetic_features(B, dev, seed=i, row0=rank * B) for i in range(nbuf)]
+    feats = bufs[0]
+    host_ids = [torch.empty(world * B, T, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+
+    def finish(i, ids):
+        """The step's tail inside the timed region: for N > 1 the one all-gather of token ids
+        (adaptive_amd.distributed.gather_rows, RCCL), then the ids device -> host copy."""
+        if world > 1:
+            ids = gather_rows(ids, world * B)
+        host_ids[i & 1].copy_(ids, non_blocking=True)
+
+    def step(i, trace=None):
+        ids, alpha, beta = model.sampler(bufs[i % nbuf], max_len=T, trace=trace, lanes=args.lanes,
+                                         graph=not args.no_graph)
+        finish(i, ids)
+
     pipe = DecodePipeline(model, max_len=T, depth=depth)
 
     def pipelined(n):
-        for ids, _, _ in pipe.run(itertools.repeat(feats, n)):
-            if world > 1:
-                dist.all_gather_into_tensor(ids_all, ids)
+        for i, (ids, _, _) in enumerate(pipe.run(bufs[i % nbuf] for i in range(n))):
+            finish(i, ids)
 
-    for _ in range(args.warmup):
-        step()
-    pipelined(max(args.warmup, 2 * depth + 1))  # every slot sees the input twice: its plan is captured
+    for i in range(max(args.warmup, 2 * nbuf)):  # every buffer seen twice: its decode plan is captured
+        step(i)
+    pipelined(max(args.warmup, 2 * depth + 1))
     K = args.steps
     traces = []
     if not args.no_trace:
@@ -199,6 +272,7 @@ def main():
             tr = _lib.Trace(ev["encoder"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["screen"].ptr, ev["rescore"].ptr,
                             ev["gemm"].ptr if model.split_lstm else None)
             traces.append((ev, tr))
+
     def timed(trace_list, pipeline=False):
         torch.cuda.synchronize()
         if world > 1:
@@ -209,7 +283,7 @@ def main():
             pipelined(K)
         else:
             for k in range(K):
-                step(trace_list[k][1] if trace_list else None)
+                step(k, trace_list[k][1] if trace_list else None)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -220,20 +294,23 @@ def main():
             el = float(tt.item())
         return el
 
-    # Region 1 (the headline): K steps with no instrumentation.  Region 2: the same K steps with a
-    # HIP event pair around every kernel launch (on the launch stream) for the per-kernel averages;
-    # each event is a timestamp packet in the queue, so region 2 runs a little slower and is
-    # reported separately as ``traced_ms_per_step``.
-    # Region 0: the same K batches through DecodePipeline (depth batches in flight) -- the headline
-    # when depth > 1; region 1 (sequential sampler calls) is reported beside it.
-    elapsed_seq = timed(None)
-    elapsed = timed(None, pipeline=True) if depth > 1 else elapsed_seq
+    # Regions: `--regions` (>= 5) timed regions of exactly K steps each for the sequential sampler
+    # calls and, when depth > 1, for DecodePipeline (the headline); value = the median region.  Then
+    # one more region of the K sequential steps with a HIP event pair around every kernel launch
+    # (on its launch stream) for the per-kernel averages; events are timestamp packets in the queue,
+    # so that region runs a little slower and is reported separately as ``traced_ms_per_step``.
+    R = max(5, args.regions)
+    seq_regions = [timed(None) for _ in range(R)]
+    log(f"sequential regions (s): {seq_regions}")
+    pipe_regions = [timed(None, pipeline=True) for _ in range(R)] if depth > 1 else seq_regions
+    log(f"pipelined regions (s): {pipe_regions}")
+    elapsed_seq = float(np.median(seq_regions))
+    elapsed = float(np.median(pipe_regions))
     traced_elapsed = timed(traces) if traces else None
     captions = world * B * K
     value = captions / elapsed
     ms_per_step = 1e3 * elapsed / K
 
-    fl = flops_per_caption(T)
     kernels = {}
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
@@ -293,6 +370,7 @@ def main():
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"]}
 
+    ideal = path_ideal_seconds(B, T)
     out = {
         "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -303,22 +381,33 @@ def main():
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
                    "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else ""),
                    "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
-                   "hip_graph": not args.no_graph, "batches_in_flight": depth,
+                   "batches_in_flight": depth, "feature_buffers": nbuf,
+                   # how each region launches: the pipeline's slots launch kernels directly (its
+                   # graph=False default); the sequential region replays captured decode plans
+                   "hip_graph": {"pipelined": pipe.graph, "sequential": not args.no_graph},
                    "lstm_step": "split (k_lstm_gemm on a side stream + k_lstm_cell)" if model.split_lstm
-                   else "fused (k_lstm)"},
-        "sequential": {"value": world * B * K / elapsed_seq, "ms_per_step": 1e3 * elapsed_seq / K,
-                       "note": "one sampler() call after another (batches_in_flight = 1)"},
+                   else "fused (k_lstm)",
+                   "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy"},
+        "regions": {"count": R, "pipelined_captions_per_s": [captions / e for e in pipe_regions],
+                    "sequential_captions_per_s": [captions / e for e in seq_regions], "reported": "median"},
+        "sequential": {"value": captions / elapsed_seq, "ms_per_step": 1e3 * elapsed_seq / K,
+                       "note": "one sampler() call after another (batches_in_flight = 1); SURVEY.md §8d's "
+                               "B / sampler wall-time"},
         "roofline": roofline,
-        "path_roofline": {"bound": "mfma", "achieved": fl["total"] * value / 1e12, "peak": PEAK_FP32 / 1e12,
-                          "unit": "TFLOP/s", "frac": fl["total"] * value / PEAK_FP32,
-                          "flops_per_caption": fl["total"],
-                          "note": "fp32-equivalent algorithmic throughput of the whole decode (SURVEY.md 8d F); "
-                                  "the vocab contraction actually runs on bf16 MFMA + exact fp32 rescoring"},
+        "path_roofline": {"bound": "per-kernel", "ideal_ms_per_batch": 1e3 * ideal["total"],
+                          "frac": 1e3 * ideal["total"] / ms_per_step,
+                          "frac_sequential": 1e3 * ideal["total"] / (1e3 * elapsed_seq / K),
+                          "ideal_ms_by_kernel": {k: 1e3 * v for k, v in ideal["parts"].items()},
+                          "note": "executed work of every kernel of one decode at its own ceiling (bf16x3 GEMMs "
+                                  "at bf16 peak/6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen over "
+                                  "all padded columns at the bf16 peak, attention / rescoring bytes at HBM "
+                                  "peak), summed, divided by the measured time per batch of 512"},
         "kernels": kernels,
         "traced_ms_per_step": None if traced_elapsed is None else 1e3 * traced_elapsed / K,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(feats.cpu(), T, args.cpu_budget)
         out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
     if rank == 0:

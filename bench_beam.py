@@ -29,7 +29,8 @@ from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
 
 def cpu_baseline(K, T, sample, budget_s):
     from oracle.adaptive_oracle import BeamOracle  # test / baseline infrastructure only
-    threads = min(16, len(os.sched_getaffinity(0)))
+    from bench import available_cpus  # every CPU this process may use (affinity capped by the cgroup quota)
+    threads = available_cpus()["usable"]
     torch.set_num_threads(threads)
     m = BeamOracle(synth.make_weights(123))
     feats = torch.from_numpy(synth.make_features(sample, seed=0))

@@ -55,7 +55,8 @@ def step(model, opt, feats, caps, lengths):
 
 def cpu_baseline(caps, lengths, B, budget_s):
     from oracle.adaptive_oracle import TrainOracle  # test / baseline infrastructure only
-    threads = min(16, len(os.sched_getaffinity(0)))
+    from bench import available_cpus  # every CPU this process may use (affinity capped by the cgroup quota)
+    threads = available_cpus()["usable"]
     torch.set_num_threads(threads)
     m = TrainOracle(synth.make_weights(123))
     feats = torch.from_numpy(synth.make_features(B, seed=0))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 10
+#define AA_ABI_VERSION 11
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -266,6 +266,22 @@ AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const
                              const int32_t* lengths, const float* dscores, int32_t N,
                              const aa_ref_grads* grads, float* dfeats, void* workspace,
                              size_t workspace_bytes, int32_t flags, aa_stream_t stream);
+
+/* ---- Decoder.forward over T > 1 teacher-forced steps -------------------------------------------
+ * decoder(V, v_g, captions, states) (baseline_attention.py:148-194 with the adaptive block,
+ * adaptive_attention.py:110-134; called with whole captions from Encoder2Decoder.forward, :225):
+ * V [B,P,H], v_g [B,E], h0 / c0 [B,H] (the states, any of the [1,B,H] / [B,1,H] views of one
+ * contiguous buffer), tokens [B][tok_ld] int64 (column t feeds step t).  Every row runs all T steps
+ * (no packing); the sentinel's h_{t-1} is 0 at t = 0 (init_hidden, :116-120).  Outputs (each may be
+ * NULL): scores [B,T,V], alpha [B,T,P], beta [B,T], h_out / c_out [B,H] = the states after step
+ * T-1.  Forward only (the training path with gradients is aa_train_forward/backward); flags:
+ * AA_TRAIN_BF16 or 0 as for aa_train_forward.  Workspace: aa_decoder_workspace_bytes. */
+AA_API size_t aa_decoder_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
+AA_API int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, const float* V, const float* v_g,
+                              const float* h0, const float* c0, int32_t B, int32_t T, const int64_t* tokens,
+                              int32_t tok_ld, float* scores, float* alpha, float* beta, float* h_out,
+                              float* c_out, void* workspace, size_t workspace_bytes, int32_t flags,
+                              aa_stream_t stream);
 
 /* ---- beam-search decode (BASELINE config 4) ------------------------------
  * Not in the reference (its for_wzn:3 lists beam search as a TODO): semantics defined here and in

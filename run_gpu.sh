@@ -11,8 +11,9 @@ ok_or_fail() {  # continue on 0 (pass) or 1 (test failures); stop on crashes/tim
 for step in "$@"; do
   case "$step" in
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok_or_fail $? smoke; tail -3 gpurun_out/smoke.log ;;
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -15 gpurun_out/pytest_gpu.log ;;
-    testsall) timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -25 gpurun_out/pytest_gpu.log ;;
+    one) timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_configs.py} -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/pytest_one.log 2>&1; ok_or_fail $? one; tail -30 gpurun_out/pytest_one.log ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -15 gpurun_out/pytest_gpu.log ;;
+    testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok_or_fail $? tests; tail -25 gpurun_out/pytest_gpu.log ;;
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
     benchq) timeout -k 10 600 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench.json 2> gpurun_out/bench.err; ok_or_fail $? bench; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err ;;
     lanes) for n in 1 2 3 4; do timeout -k 10 300 python bench.py --no-cpu-baseline --no-trace --lanes $n ${LANES_ARGS:-} > gpurun_out/bench_l$n.json 2>> gpurun_out/bench.err; ok_or_fail $? lanes$n; python -c "import json;d=json.load(open('gpurun_out/bench_l$n.json'));print('lanes $n', round(d['value']), 'captions/s', round(d['ms_per_step'],3),'ms')"; done ;;

@@ -88,3 +88,24 @@ def test_checkpoint_round_trip_reference_names(tmp_path):
 def test_start_epoch_parsing_matches_reference():
     assert start_epoch("models/adaptive-7.pkl") == 8
     assert start_epoch("/x/y/cider-1.0312_model-12.pkl") == 2   # the reference's own quirk
+
+
+def test_checkpoint_with_trunk_loads_strictly_in_reference_shaped_module(tmp_path):
+    """A trunk-less model's file plus a torchvision-layout trunk state (save_checkpoint(...,
+    trunk_state=)) is complete: a reference-shaped module (the trunk included, as
+    model_factory.py:16 builds it) loads it with strict=True; without trunk_state it does not."""
+    from adaptive_amd.trunk import resnet_conv
+    m = Encoder2Decoder(Config()).load_synthetic(5)
+    trunk = resnet_conv()
+    full = save_checkpoint(m, str(tmp_path), 0.5, 1, trunk_state=trunk.state_dict())
+    ref_shaped = Encoder2Decoder(Config(), trunk=True)
+    load_checkpoint(ref_shaped, full, strict=True)
+    for k, v in m.state_dict().items():
+        assert torch.equal(ref_shaped.state_dict()[k], v), k
+    for k, v in trunk.state_dict().items():
+        assert torch.equal(ref_shaped.state_dict()["encoder.resnet_conv." + k], v), k
+    bare = save_checkpoint(m, str(tmp_path), 0.5, 2)
+    with pytest.raises(RuntimeError, match="Missing key"):
+        load_checkpoint(Encoder2Decoder(Config(), trunk=True), bare, strict=True)
+    with pytest.raises(ValueError):
+        save_checkpoint(ref_shaped, str(tmp_path), 0.5, 3, trunk_state=trunk.state_dict())

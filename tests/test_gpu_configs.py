@@ -1,0 +1,232 @@
+"""BASELINE configs 3 and 5 at their own sizes, and the product's multi-rank decode, on the GPU.
+
+* Config 5 (training step, B = 128, T = 18): the teacher-forced forward + CE + backward through the
+  C-ABI (aa_train_forward / aa_train_backward), bf16 GEMMs and fp32 GEMMs, against the CPU oracle's
+  autograd (``TrainOracle``, pinned to the reference's own training goldens in tests/test_oracle.py),
+  and three train.py:197-219 closure steps (zero_grad, forward, CE, backward, clip_grad_norm_(LSTM,
+  5), Adam) against the same closure on the oracle.
+* Config 3 (B = 4096): one B = 4096 decode is bitwise the concatenation of the eight B = 512 row
+  blocks decoded separately (what each of 8 ranks computes), and equals the oracle on rows sampled
+  from every block.
+* The product's multi-rank path (``Encoder2Decoder.sharded_sampler`` / ``distributed_sampler`` over
+  ``adaptive_amd.distributed``): 2 processes on the one GPU with ``gloo``, and 1 process with
+  ``nccl`` (RCCL: the ``all_gather_into_tensor`` branch), each equal to the one-process decode.
+* ``decoder(V, v_g, captions, states)`` with whole captions (T > 1, aa_decoder_forward) against the
+  oracle's ``Decoder.forward``.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+import torch.multiprocessing as mp
+from torch.nn.utils.rnn import pack_padded_sequence
+
+from adaptive_amd import Config, Encoder2Decoder, synth
+from adaptive_amd.adaptive_attention import synthetic_features
+
+pytestmark = pytest.mark.gpu
+
+# fp32 GEMMs: the tolerances of tests/test_gpu_train.py (same arithmetic, larger batch)
+SCORE_TOL, LOSS_REL, GRAD_REL, GRAD_ENTRY = 1e-4, 1e-5, 1e-3, 1e-2
+# bf16 GEMMs (AA_TRAIN_BF16): the tolerances of test_train_bf16_vs_oracle
+BF16_SCORE_REL, BF16_LOSS_REL, BF16_GRAD_REL = 2e-2, 1e-3, 5e-2
+
+
+def _config5_batch(B=128, T=18, seed=0):
+    """bench_train.py's batch: lengths T .. T/2 sorted descending, <start> first."""
+    rng = np.random.default_rng(seed)
+    lengths = sorted(rng.integers(T // 2, T + 1, size=B).tolist(), reverse=True)
+    lengths[0] = T
+    caps = rng.integers(2, 10123, size=(B, T + 1)).astype(np.int64)
+    caps[:, 0] = 1
+    return caps, lengths
+
+
+def _gpu_loss(model, feats, caps, lengths):
+    packed = model(feats, caps, lengths)
+    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]
+    return F.cross_entropy(packed[0], targets), packed
+
+
+@pytest.fixture(scope="module")
+def config5():
+    from oracle.adaptive_oracle import TrainOracle
+    caps, lengths = _config5_batch()
+    state = synth.make_weights(123, bias_noise=0.02)
+    feats = synth.make_features(128, seed=0)
+    oracle = TrainOracle(state)
+    loss, packed = oracle.loss(torch.from_numpy(feats), torch.from_numpy(caps), lengths)
+    loss.backward()
+    grads = {k: v.grad.detach().double().numpy() for k, v in oracle.w.items()}
+    return caps, lengths, feats, loss.item(), packed[0].detach().double().numpy(), grads
+
+
+@pytest.mark.parametrize("bf16", [True, False])
+def test_config5_train_step_b128_t18_vs_oracle(config5, gpu_device, bf16):
+    caps_np, lengths, feats_np, rloss, rscores, rgrads = config5
+    model = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123, bias_noise=0.02)
+    model.train_bf16 = bf16
+    loss, packed = _gpu_loss(model, torch.from_numpy(feats_np).to(gpu_device),
+                             torch.from_numpy(caps_np).to(gpu_device), lengths)
+    assert packed[0].shape == (sum(lengths), 10123)
+    got = packed[0].detach().cpu().double().numpy()
+    loss.backward()
+    if bf16:
+        assert np.linalg.norm(got - rscores) <= BF16_SCORE_REL * np.linalg.norm(rscores)
+        assert abs(loss.item() - rloss) <= BF16_LOSS_REL * abs(rloss)
+    else:
+        assert np.abs(got - rscores).max() <= SCORE_TOL
+        assert abs(loss.item() - rloss) <= LOSS_REL * abs(rloss)
+    for k, p in model.named_parameters():
+        g, r = p.grad.detach().cpu().double().numpy(), rgrads[k]
+        if bf16:
+            assert np.linalg.norm(g - r) <= BF16_GRAD_REL * max(np.linalg.norm(r), 1e-30), k
+        else:
+            assert np.abs(g - r).max() <= GRAD_ENTRY * max(np.abs(r).max(), 1e-30), k
+            assert np.linalg.norm(g - r) <= GRAD_REL * max(np.linalg.norm(r), 1e-30), k
+
+
+def test_config5_adam_clip_closure_vs_oracle(config5, gpu_device):
+    """train.py:197-219 three times at config 5 (bf16 GEMMs) beside the same closure on the oracle:
+    per-step loss and the LSTM gradient norm that clip_grad_norm_ reports agree within the bf16
+    tolerances, and the loss goes down."""
+    from oracle.adaptive_oracle import TrainOracle
+    caps_np, lengths, feats_np, _, _, _ = config5
+    oracle = TrainOracle(synth.make_weights(123, bias_noise=0.02))
+    o_opt = torch.optim.Adam(list(oracle.w.values()), lr=1e-3)
+    o_lstm = [oracle.w["decoder.LSTM." + n] for n in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0")]
+    model = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123, bias_noise=0.02)
+    model.train_bf16 = True
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    feats, caps = torch.from_numpy(feats_np).to(gpu_device), torch.from_numpy(caps_np).to(gpu_device)
+    of, oc = torch.from_numpy(feats_np), torch.from_numpy(caps_np)
+    losses = []
+    for _ in range(3):
+        model.zero_grad()
+        opt.zero_grad()
+        loss, _ = _gpu_loss(model, feats, caps, lengths)
+        loss.backward()
+        norm = torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+        opt.step()
+        o_opt.zero_grad()
+        rloss, _ = oracle.loss(of, oc, lengths)
+        rloss.backward()
+        rnorm = torch.nn.utils.clip_grad_norm_(o_lstm, 5.0)
+        o_opt.step()
+        assert abs(loss.item() - rloss.item()) <= 2 * BF16_LOSS_REL * abs(rloss.item())
+        assert abs(norm.item() - rnorm.item()) <= BF16_GRAD_REL * rnorm.item()
+        losses.append(loss.item())
+    assert losses[2] < losses[1] < losses[0]
+    for p in model.parameters():
+        assert torch.isfinite(p).all()
+
+
+def test_config3_b4096_equals_eight_b512_blocks(gpu_device):
+    """One B = 4096 decode == the eight 512-row blocks decoded separately (bitwise: ids, alpha,
+    beta), i.e. what 8 ranks of the sharded decode compute; rows sampled from every block == the
+    oracle (their top-2 logit margins are asserted well above the fp32 logit differences)."""
+    from oracle.adaptive_oracle import OracleModel, top2_margin
+    m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
+    feats = synthetic_features(4096, gpu_device, seed=0)
+    full = m.sampler(feats, max_len=20, graph=False)
+    for k in range(8):
+        blk = m.sampler(feats[512 * k: 512 * (k + 1)].contiguous(), max_len=20, graph=False)
+        for a, b in zip(full, blk):
+            assert torch.equal(a[512 * k: 512 * (k + 1)], b), k
+    rows = [512 * k + o for k in range(8) for o in (0, 137, 300, 511)]
+    fr = np.concatenate([synth.make_features(1, seed=0, row0=r) for r in rows])
+    assert torch.equal(feats[rows].cpu(), torch.from_numpy(fr))
+    o_ids, o_al, o_be, o_sc = OracleModel(synth.make_weights(123)).sampler(torch.from_numpy(fr), max_len=20,
+                                                                            keep_scores=True)
+    assert top2_margin(o_sc).min().item() > 1e-5
+    assert torch.equal(full[0][rows].cpu(), o_ids)
+    np.testing.assert_allclose(full[1][rows].cpu().numpy(), o_al.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(full[2][rows].cpu().numpy(), o_be.numpy(), atol=2e-5, rtol=0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_worker(rank, world, port, backend, total, T, q):
+    """One rank of the product's sharded decode on cuda:0."""
+    import torch.distributed as dist
+    from adaptive_amd.distributed import shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+        lo, hi = shard_bounds(total, world, rank)
+        local = synthetic_features(hi - lo, dev, seed=0, row0=lo)  # each rank makes only its rows
+        a = m.sharded_sampler(local, max_len=T, total=total)
+        m.distributed_sampler = True  # opt-in: sampler() itself shards a batch every rank holds
+        b = m.sampler(synthetic_features(total, dev, seed=0), max_len=T)
+        torch.cuda.synchronize()
+        if rank == 0:
+            q.put(tuple(x.cpu() for x in a + b))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend,world,total", [("gloo", 2, 1031), ("nccl", 1, 512)])
+def test_sharded_sampler_processes_equal_one_process(gpu_device, backend, world, total):
+    T = 20
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, backend, total, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
+    ref = m.sampler(synthetic_features(total, gpu_device, seed=0), max_len=T, graph=False)
+    for x, r in zip(got, ref + ref):
+        assert torch.equal(x, r.cpu())
+
+
+def test_decoder_whole_captions_vs_oracle(gpu_device):
+    """decoder(V, v_g, captions, states) with T = 12-token captions (Decoder.forward as
+    Encoder2Decoder.forward calls it, baseline_attention.py:225) against the oracle's Decoder.forward
+    on the same V, v_g and states."""
+    from oracle.adaptive_oracle import OracleModel
+    B, T = 9, 12
+    m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(31, bias_noise=0.01)
+    feats = torch.from_numpy(synth.make_features(B, seed=5)).to(gpu_device)
+    V, v_g, (h0, c0) = m.encoder(feats)
+    rng = np.random.default_rng(3)
+    caps = torch.from_numpy(rng.integers(0, 10123, size=(B, T)).astype(np.int64))
+    caps[:, 0] = 1
+    states = (h0.transpose(0, 1), c0.transpose(0, 1))  # [1,B,H], as Encoder2Decoder.forward passes them
+    sc, al, be, (h, c) = m.decoder(V, v_g, caps.to(gpu_device), states)
+    assert sc.shape == (B, T, 10123) and al.shape == (B, T, 49) and be.shape == (B, T, 1)
+    assert h.shape == (1, B, 512) and c.shape == (1, B, 512)
+    o = OracleModel(synth.make_weights(31, bias_noise=0.01))
+    with torch.no_grad():
+        osc, oal, obe, (oh, oc) = o.decoder(V.cpu(), v_g.cpu(), caps, (states[0].cpu().contiguous(),
+                                                                     states[1].cpu().contiguous()))
+    np.testing.assert_allclose(sc.cpu().numpy(), osc.numpy(), atol=SCORE_TOL, rtol=0)
+    np.testing.assert_allclose(al.cpu().numpy(), oal.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(be.cpu().numpy(), obe.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(h.cpu().numpy(), oh.numpy(), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(c.cpu().numpy(), oc.numpy(), atol=1e-5, rtol=0)
+    # one-token captions still run the sampling step (sentinel h_{t-1} = 0) and agree with T = 1 here
+    sc1, al1, be1, _ = m.decoder(V, v_g, caps[:, :1].to(gpu_device), states)
+    np.testing.assert_allclose(sc1.cpu().numpy(), sc[:, :1].cpu().numpy(), atol=SCORE_TOL, rtol=0)
+    with pytest.raises(IndexError):
+        m.decoder(V, v_g, torch.full((B, 3), 10123, dtype=torch.int64, device=gpu_device), states)

@@ -38,3 +38,23 @@ def test_pipeline_repeated_input_uses_plans(model, gpu_device, depth):
     for out in outs:
         for a, b in zip(out, ref):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_pipeline_fp32_encoder_equals_sampler(gpu_device, graph):
+    """The pipeline passes the same decode flags as sampler(): with fp32_encoder the V GEMM runs on
+    fp32 MFMA in both (the pipeline used to drop the flag)."""
+    m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
+    m.fp32_encoder = True
+    f = synthetic_features(96, gpu_device, seed=12)
+    ref = m.sampler(f, max_len=10, graph=False)
+    m.fp32_encoder = False
+    other = m.sampler(f, max_len=10, graph=False)
+    m.fp32_encoder = True
+    pipe = DecodePipeline(m, max_len=10, depth=2, graph=graph)
+    outs = list(pipe.run([f] * 5))
+    for out in outs:
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+    # the encoders really differ (alpha is sensitive to V's last bits), so the check above has teeth
+    assert not torch.equal(ref[1], other[1])
