@@ -9,6 +9,23 @@
 
 namespace aa {
 
+// Phase timestamps for tools/ktrace (an instrumented build only: -DAA_TS_ENABLE): thread 0 of each
+// workgroup writes s_memrealtime (100 MHz) to aa_ts_buf[kernel][blockIdx.x][slot].  Empty in the
+// product build.
+#ifdef AA_TS_ENABLE
+__device__ uint64_t* aa_ts_buf = nullptr;
+__device__ __forceinline__ void aa_ts(int kid, int slot) {
+  if (threadIdx.x == 0 && aa_ts_buf) {
+    uint64_t* p = aa_ts_buf + ((size_t)kid * 2048 + blockIdx.x) * 16 + slot;
+    p[0] = __builtin_amdgcn_s_memrealtime();
+    p[8] = __builtin_amdgcn_s_memtime();  // shader clock: (memtime delta) / (realtime delta) = clock
+  }
+}
+#define AA_TS(kid, slot) aa_ts(kid, slot)
+#else
+#define AA_TS(kid, slot)
+#endif
+
 constexpr int P = 49;          // attention width == 7x7 spatial locations (adaptive_attention.py:16-19)
 constexpr int PP = 64;         // padded attention width (VWv row pitch, W_v rows)
 constexpr int MAX_H = 1024;    // kernels keep h / s / u rows in LDS

@@ -413,6 +413,16 @@ __global__ __launch_bounds__(256, 2) void k_enc_v3(const float* __restrict__ fea
 // LDS as [image][channel][p], and one wave per stage (rotating) sums every channel of both images
 // sequentially in p order and divides by 49 -- k_avgpool's arithmetic, bit-identical to ATen.
 // ---------------------------------------------------------------------------------------------
+// The feature map is read once per batch: non-temporal loads (AA_FEAT_NT=1) keep the 205 MB stream from
+// evicting the step kernels' working set (V, W_m, the token table) of the batches in flight.
+#ifndef AA_FEAT_NT
+#define AA_FEAT_NT 1
+#endif
+#if AA_FEAT_NT
+#define AA_FEAT_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define AA_FEAT_LOAD(p) (*(p))
+#endif
 constexpr int E4_ROWS = 98, E4_RB = 7, E4_LD = 48;  // rows per workgroup, 16-row blocks, LDS pitch (bf16)
 constexpr int E4_SP = 52, E4_MAXC = 2048;           // a_g staging pitch (floats), largest channel count
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -452,7 +462,7 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
   auto gload_a = [&](int s) {
     const float* src = arow + (int64_t)(32 * s) * P;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ra[i] = src[i * P];
+    for (int i = 0; i < 8; ++i) ra[i] = AA_FEAT_LOAD(src + i * P);
   };
   auto gload_w = [&](int s, int c) {
 #pragma unroll
@@ -804,6 +814,7 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
       }
     }
   }
+  AA_TS(0, 3);
   __syncthreads();
   // Wave -> one 32x32 block: rows rb*32.., columns cb = 0, 1: W_g j = 0..63; cb = 2, 3: W_s j = 0..63.
   {
@@ -918,10 +929,16 @@ __device__ __forceinline__ void lstm_gemm_partials(const bf16x8* af0, const bf16
 // (one from each batch in flight) where the 8-partial version claims the whole CU.  Each fragment
 // is loaded by the two waves that share it (twice the L2 reads).  The K halves are summed as
 // (lower + upper) into the single tile Pt [column][row]; the caller reads it after a barrier.
+#ifndef AA_LSTM_NR
+#define AA_LSTM_NR 2
+#endif
+#ifndef AA_LSTM_OCC
+#define AA_LSTM_OCC 4
+#endif
 template <int H, class F>
 __device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
                                                const bf16x8* wf1, float* Pt, F&& between) {
-  constexpr int KC = H / 16, CP = LS_CP, per = KC / 2, NR = 2;
+  constexpr int KC = H / 16, CP = LS_CP, per = KC / 2, NR = AA_LSTM_NR;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
   const bf16x8* af = a ? af1 : af0;
@@ -948,10 +965,133 @@ __device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* 
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < per; ++i) {
+#ifdef AA_EXP_NOMFMA  // tools/ktrace experiment: loads only (wrong results)
+    acc[0] += (float)fa[i % NR][0][0] + (float)fw[i % NR][0][0];
+#else
     x3_step(acc, fa[i % NR], fw[i % NR]);
+#endif
+#ifndef AA_EXP_NOLOAD  // tools/ktrace experiment: MFMAs on the first NR chunks only (wrong results)
     if (i + NR < per) load(i % NR, kc0 + i + NR);
+#endif
     __builtin_amdgcn_sched_barrier(0);
   }
+  const int li = lane & 31, lh = lane >> 5;
+  float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;
+  if (kh) {
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4)
+      *reinterpret_cast<float4*>(dst + 8 * r4) = make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
+  }
+  __syncthreads();
+  if (!kh) {
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      float4* e = reinterpret_cast<float4*>(dst + 8 * r4);
+      const float4 v = *e;
+      *e = make_float4(acc[4 * r4] + v.x, acc[4 * r4 + 1] + v.y, acc[4 * r4 + 2] + v.z, acc[4 * r4 + 3] + v.w);
+    }
+  }
+}
+
+// LDS-staged variant of the lean GEMM (the default): the same waves, blocks, K halves, chunk order
+// and MFMA sequence (bit-identical accumulators), but every fragment reaches LDS ONCE per workgroup by
+// LDS-DMA (global_load_lds, 1 KB per wave instruction) and the two waves that share it read it
+// from there.  The register-staged lean GEMM loads each fragment twice (768 KB per workgroup where
+// 384 KB are unique): its fragment stream was the GEMM phase's bound (tools/ktrace: loads alone 5.0
+// of the 8.9 us).  A stage = chunk `it` of both K halves = 24 fragments (24 KB): fragment f = 12 kh
+// + j, j < 6: A row block j / 3, plane j % 3; j >= 6: W column block (j - 6) / 3, plane (j - 6) % 3.
+// Wave w issues fragments 3w .. 3w + 2 of every stage.  Three stages in a ring: stage it + 2 is in
+// flight while stage it is multiplied (counted vmcnt, raw s_barrier: a __syncthreads() would drain
+// the DMAs).  `pre` runs after the first three stages are issued: it may issue exactly LS_GATHERS
+// ordinary loads (the cell's gathers), which the counted waits of the first two iterations account
+// for.  Ends with the K halves summed into Pt [column][row] (Pt aliases the ring).
+#ifndef AA_LSTM_NB
+#define AA_LSTM_NB 3
+#endif
+constexpr int LS_NB = AA_LSTM_NB;             // ring stages (LS_NB - 1 in flight ahead of the one multiplied)
+constexpr int LS_STAGE = 24 * 64;             // bf16x8 per stage
+constexpr int LS_GATHERS = 12;                // ordinary loads issued by k_lstm's gathers (ISA-checked)
+
+// s_waitcnt vmcnt(n) for an n that is a compile-time constant once the caller's loop is unrolled
+template <int V>
+__device__ __forceinline__ void vm_wait_c() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory"); }
+template <int V = 0>
+__device__ __forceinline__ void vm_wait(int n) {
+  if constexpr (V < 63) {
+    if (n == V) vm_wait_c<V>();
+    else vm_wait<V + 1>(n);
+  } else {
+    vm_wait_c<63>();
+  }
+}
+
+template <int H, class F>
+__device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
+                                              const bf16x8* wf1, bf16x8* stg, float* Pt, F&& pre) {
+  constexpr int KC = H / 16, CP = LS_CP, N = KC / 2, NB = LS_NB < N ? LS_NB : N;
+  static_assert(NB >= 3, "the ring needs at least three stages");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
+  const bf16x8* src[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int f = 3 * wave + i, hf = f / 12, j = f % 12;
+    const bf16x8* base = j < 6 ? (j < 3 ? af0 : af1) : (j < 9 ? wf0 : wf1);
+    src[i] = base + (size_t)(hf * N * 3 + (j % 3)) * 64;  // + it * 3 * 64 per stage
+  }
+  auto issue = [&](int it) {
+    bf16x8* dst = stg + (it % NB) * LS_STAGE + (3 * wave) * 64;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)it * 3 * 64),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 64), 16, 0, 0);
+  };
+  bf16x8 fa[2][3], fw[2][3];
+  auto lread = [&](int it, int set) {
+    const bf16x8* sb = stg + (it % NB) * LS_STAGE + kh * 12 * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      fa[set][q] = sb[(3 * a + q) * 64];
+      fw[set][q] = sb[(6 + 3 * c + q) * 64];
+    }
+  };
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int it = 0; it < NB; ++it) issue(it);
+  __builtin_amdgcn_sched_barrier(0);
+  pre();  // waits for its own older loads with vmcnt(3 NB); issues exactly LS_GATHERS loads
+  __builtin_amdgcn_sched_barrier(0);
+  // stage 0 landed (younger: stages 1 .. NB-1 and the gathers)
+  vm_wait(3 * (NB - 1) + LS_GATHERS);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  lread(0, 0);
+#pragma unroll
+  for (int it = 0; it < N; ++it) {
+    const int set = it & 1;
+    if (it + 1 < N) {
+      // stage it + 1 landed: younger are the stages issued after it (up to it + NB - 1) and, while
+      // it + 1 <= NB - 1, the gathers (issued after stage NB - 1)
+      const int last = it + NB - 1 < N - 1 ? it + NB - 1 : N - 1;
+      vm_wait(3 * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0));
+      // every wave's stage-it reads retired (lgkmcnt) before any wave refills that buffer
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifndef AA_EXP_NOLOAD
+      if (it + NB < N) issue(it + NB);
+#endif
+      lread(it + 1, set ^ 1);
+    }
+#ifdef AA_EXP_NOMFMA
+    acc[0] += (float)fa[set][0][0] + (float)fw[set][0][0];
+#else
+    x3_step(acc, fa[set], fw[set]);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ring free: Pt aliases it
   const int li = lane & 31, lh = lane >> 5;
   float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;
   if (kh) {
@@ -974,7 +1114,7 @@ __device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* 
 // fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
 // gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
 template <int H, bool G = false, bool LEAN = true>
-__global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+__global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
                                               const float* __restrict__ c_in, const int* __restrict__ par,
@@ -983,7 +1123,12 @@ __global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const 
                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
                                               float* __restrict__ s_out, float* __restrict__ part) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
-  __shared__ __attribute__((aligned(16))) float lds[(LEAN ? 1 : 4) * TS + LS_TAIL_FLOATS];
+  AA_TS(0, 0);
+  // LEAN: the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
+  constexpr int RING_FLOATS = (LS_NB < H / 32 ? LS_NB : H / 32) * LS_STAGE * 4;
+  constexpr int LDS_FLOATS = LEAN ? RING_FLOATS + 64 : 4 * TS + LS_TAIL_FLOATS;  // + the tile's 64 tokens
+  static_assert(!LEAN || TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, MT * NTn);
@@ -996,7 +1141,20 @@ __global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const 
   const int j = nt * 16 + u0;
   // (token first, then the GEMM's first loads, then the token-dependent gathers: in-order vmcnt
   //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
-  int64_t tk = tok[(int64_t)mc * tok_ld];
+  int64_t tk = 0;
+  int* tok_lds = reinterpret_cast<int*>(lds + RING_FLOATS);
+  if constexpr (LEAN) {
+    // the tile's 64 tokens by ONE LDS-DMA of wave 0 (the low dword of each int64 token), so that no
+    // ordinary load is outstanding beside the ring's DMAs: hipcc drains every DMA (vmcnt(0)) before
+    // the first use of an ordinary load's result while a DMA is in flight
+    if (t < 64) {
+      const int r = m0 + t < B ? m0 + t : B - 1;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tok + (int64_t)r * tok_ld),
+                                       (__attribute__((address_space(3))) void*)tok_lds, 4, 0, 0);
+    }
+  } else {
+    tk = tok[(int64_t)mc * tok_ld];
+  }
   const bf16x8* af0;
   const bf16x8* af1;
   int pc = mc;  // source row of c (and of h, through the fragments)
@@ -1034,7 +1192,19 @@ __global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const 
     wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
   };
   if constexpr (LEAN) {
-    lstm_gemm_lean<H>(af0, af1, wf0, wf1, Pt, gathers);
+    // token first (oldest), then the ring's first three stages, then -- once the token is in --
+    // the token-dependent gathers (exactly LS_GATHERS loads, counted by the ring's waits)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
+      // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
+      if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      tk = tok_lds[rr];
+      gathers();
+      asm volatile("" ::: "memory");
+    });
+    AA_TS(0, 1);
   } else {
     lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, gathers);
     __syncthreads();
@@ -1060,7 +1230,9 @@ __global__ __launch_bounds__(512, LEAN ? 4 : 1) void k_lstm(int B, int V, const 
 #pragma unroll
       for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
   }
+  AA_TS(0, 2);
   lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + (LEAN ? 1 : 4) * TS, h_out, hsp_out, c_out, s_out, part);
+  AA_TS(0, 4);
 }
 
 // Split LSTM step, part 1: G = h_{t-1} W_hh^T (the tile of k_lstm, same lean partials and order) written
@@ -1336,6 +1508,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   __shared__ float sh_alpha[PP];
   __shared__ float sh_beta;
   __shared__ float sh_norm[8];
+  AA_TS(1, 0);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
@@ -1377,6 +1550,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
     red[grp][jp] = a;
   }
   __syncthreads();
+  AA_TS(1, 1);
   if (t < 2 * P) proj[t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
   __syncthreads();
   // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
@@ -1394,6 +1568,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
     if (q == 0 && k <= P) zs[k] = z;
   }
   __syncthreads();
+  AA_TS(1, 2);
   // 3) softmax (wave 0)
   if (w == 0) {
     const float z = lane < P ? zs[lane] : -INFINITY;
@@ -1417,6 +1592,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
     }
   }
   __syncthreads();
+  AA_TS(1, 3);
   // 4) context + u
   const float beta = sh_beta;
   float nsq = 0.f;
@@ -1449,6 +1625,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
       unorm[b] = sqrtf(((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) +
                        ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.00001f;
   }
+  AA_TS(1, 4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1682,6 +1859,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
   __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
   __shared__ float un_s[SC2_BM];
+  AA_TS(2, 0);
   const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
   const int L = xcd_remap(blockIdx.x, MT * NT);
   const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
@@ -1743,6 +1921,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
       }
     }
   }
+  AA_TS(2, 1);
   const float bvs[SC2_NB] = {bv0, bv1, bv2, bv3, bv4};
   const int row0 = m0 + 32 * wave;
 #pragma unroll
@@ -1750,6 +1929,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
     const int G = n0 / VS_TILE + b;
     screen_block_summ(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
   }
+  AA_TS(2, 2);
 }
 
 // Exact fp32 logit of one column, computed by a group of 8 lanes (lane8 = 0..7): lane8 j runs the
@@ -1796,6 +1976,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
   __shared__ int ncand;
   __shared__ float wmax[4];
   __shared__ uint64_t wbest[4];
+  AA_TS(3, 0);
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int NTn = Vp / VS_TILE;
   for (int d = 4 * t; d < H; d += 1024) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
@@ -1806,6 +1987,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
   mlb = wave_max(mlb);
   if (lane == 0) wmax[w] = mlb;
   __syncthreads();
+  AA_TS(3, 1);
   mlb = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
   for (int i = t; i < NTn; i += 256) {
     const float4 s = sm[i];
@@ -1819,6 +2001,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
     }
   }
   __syncthreads();
+  AA_TS(3, 2);
   const bool all = ncand > RS_CAP;
   const int n = all ? V : ncand;
   const int g = t >> 3, lane8 = t & 7;
@@ -1842,6 +2025,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
     keys[b] = k;
     if (ids) ids[(int64_t)b * T + t_step] = key_token(k);
   }
+  AA_TS(3, 3);
 }
 
 // Exact fp32 logits of selected columns (cols [B][n], -1 = skip) -> out [B][n]; same arithmetic.
@@ -2047,6 +2231,11 @@ static void gemm_bias(const float* A, int lda, int M, const float* W, int ldw, i
 }
 
 int aa_abi_version(void) { return AA_ABI_VERSION; }
+#ifdef AA_TS_ENABLE
+extern "C" __attribute__((visibility("default"))) int aa_ts_setup(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(aa_ts_buf), &buf, sizeof(buf));
+}
+#endif
 
 const char* aa_error_string(int code) {
   switch (code) {

@@ -211,6 +211,11 @@ def main():
                     "128x160 (k_vscreen2)")
     ap.add_argument("--enc-v3", action="store_true", help="encoder V GEMM on k_enc_v3 (128x128 tiles) instead of "
                     "k_enc_v4 (two images per workgroup, all columns)")
+    ap.add_argument("--no-d2h", action="store_true", help="diagnostics: leave the ids on the device (not the metric)")
+    ap.add_argument("--single-buffer", action="store_true", help="diagnostics: every batch reads the same feature "
+                    "buffer (MALL-resident; not the metric)")
+    ap.add_argument("--replicate-buffer", action="store_true", help="diagnostics: distinct feature buffers holding "
+                    "copies of the same batch (not the metric)")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -237,9 +242,12 @@ def main():
     # map, so nothing is served from the 256 MB MALL left behind by the previous batch.  Buffer 0 is
     # the canonical batch (rows [rank B, (rank+1) B) of the seed-0 global batch); the others use
     # seeds 1.. for the same rows.
-    nbuf = max(depth, 2)
+    nbuf = 1 if args.single_buffer else max(depth, 2)
     bufs = [synthetic_features(B, dev, seed=i, row0=rank * B) for i in range(nbuf)]
     feats = bufs[0]
+    if args.replicate_buffer:
+        for b_ in bufs[1:]:
+            b_.copy_(feats)
     host_ids = [torch.empty(world * B, T, dtype=torch.int64, pin_memory=True) for _ in range(2)]
 
     def finish(i, ids):
@@ -247,7 +255,8 @@ def main():
         (adaptive_amd.distributed.gather_rows, RCCL), then the ids device -> host copy."""
         if world > 1:
             ids = gather_rows(ids, world * B)
-        host_ids[i & 1].copy_(ids, non_blocking=True)
+        if not args.no_d2h:
+            host_ids[i & 1].copy_(ids, non_blocking=True)
 
     def step(i, trace=None):
         ids, alpha, beta = model.sampler(bufs[i % nbuf], max_len=T, trace=trace, lanes=args.lanes,

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_$tag
 for p in $passes; do
   case $p in
-    sq)    ctr="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" ;;
+    sq)    ctr="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" ;;
     mfma)  ctr="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" ;;
     fetch) ctr="FETCH_SIZE" ;;
     write) ctr="WRITE_SIZE" ;;
