@@ -428,14 +428,20 @@ class Encoder2Decoder(nn.Module):
 
     @torch.no_grad()
     def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2,
-                    exact_vocab: bool = False):
+                    exact_vocab: Optional[bool] = None, fast: bool = False):
         """Beam-search decode (BASELINE config 4; not in the reference, semantics in
         include/adaptive_amd.h and DESIGN.md) -> (ids [B,T], alpha [B,T,49], beta [B,T,1],
         seqs [B,K,T], scores [B,K]): ids / alpha / beta of the best final beam, then every final
         beam best first with its cumulative log-probability.  ``end_id`` = the vocabulary's
         ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables.
-        ``exact_vocab``: logits from the fp32 MFMA GEMM instead of the default bf16x3 GEMM with
-        fused log-sum-exp summaries (both fp32-accurate)."""
+        Logits are exact fp32 (the fp32 MFMA GEMM's fma chains, as the greedy path's exact mode) by
+        default; ``fast=True`` (or the older ``exact_vocab=False``) computes them by bf16x3 MFMA with
+        fused log-sum-exp summaries -- fp32-accurate but not bitwise, so a near-tie between two
+        candidates can be decided differently (opt-in speed mode)."""
+        if exact_vocab is not None:
+            if exact_vocab and fast:
+                raise ValueError("exact_vocab=True contradicts fast=True")
+            fast = not exact_vocab
         images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
@@ -455,7 +461,7 @@ class Encoder2Decoder(nn.Module):
             rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
                                     ws.numel() if ws is not None else 0,
-                                    (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0)
+                                    (_lib.BEAM_FAST if fast else 0)
                                     | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle())
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores

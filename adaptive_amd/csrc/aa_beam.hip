@@ -57,100 +57,6 @@ __device__ __forceinline__ uint64_t block_max256_u64(uint64_t v, uint64_t* red) 
   return a > c ? a : c;
 }
 
-// One workgroup per image.  logits [R][V] (R = B*K); cum / fin [R] updated in place; tok / par
-// [R] = the next step's input token and parent row; htok / hpar [T][R] = history (hpar local).
-__global__ __launch_bounds__(256) void k_beam_select(int K, int V, int R, int t, int end_id,
-                                                     const float* __restrict__ logits, float* __restrict__ cum,
-                                                     int* __restrict__ fin, int64_t* __restrict__ tok,
-                                                     int* __restrict__ par, int* __restrict__ htok,
-                                                     int* __restrict__ hpar) {
-  __shared__ float redf[4];
-  __shared__ uint64_t redk[4];
-  __shared__ float s_mx[BEAM_MAX], s_ls[BEAM_MAX];
-  __shared__ uint64_t s_top[BEAM_MAX][BEAM_MAX];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  for (int k = 0; k < K; ++k) {
-    const int row = b * K + k;
-    const bool live = !(t == 0 && k > 0) && !(fin[row] != 0);  // uniform over the workgroup
-    if (!live) continue;
-    const float* x = logits + (int64_t)row * V;
-    float xs[BEAM_VPT];
-#pragma unroll
-    for (int i = 0; i < BEAM_VPT; ++i) {
-      const int c = tid + 256 * i;
-      xs[i] = c < V ? x[c] : -INFINITY;
-    }
-    float m = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < BEAM_VPT; ++i) m = fmaxf(m, xs[i]);
-    m = block_max256(m, redf);
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < BEAM_VPT; ++i)
-      if (tid + 256 * i < V) sum += expf(xs[i] - m);
-    sum = block_sum256(sum, redf);
-    if (tid == 0) {
-      s_mx[k] = m;
-      s_ls[k] = logf(sum);
-    }
-    // top-K of the row by (logit desc, column asc): K rounds of a block arg-max below the last key
-    uint64_t prev = ~0ull;
-    for (int j = 0; j < K; ++j) {
-      uint64_t best = 0;
-#pragma unroll
-      for (int i = 0; i < BEAM_VPT; ++i) {
-        const int c = tid + 256 * i;
-        const uint64_t key = c < V ? argmax_key(xs[i], c) : 0ull;
-        if (key < prev && key > best) best = key;
-      }
-      best = block_max256_u64(best, redk);
-      if (tid == 0) s_top[k][j] = best;
-      prev = best;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float ocum[BEAM_MAX];
-    int ofin[BEAM_MAX];
-    for (int k = 0; k < K; ++k) {
-      ocum[k] = cum[b * K + k];
-      ofin[k] = fin[b * K + k];
-    }
-    float cv[BEAM_MAX * BEAM_MAX];
-    int cf[BEAM_MAX * BEAM_MAX];
-    int n = 0;
-    for (int k = 0; k < K; ++k) {
-      if (t == 0 && k > 0) continue;
-      if (ofin[k]) {
-        cv[n] = ocum[k];
-        cf[n++] = k * V + end_id;
-        continue;
-      }
-      for (int j = 0; j < K; ++j) {
-        const int col = (int)key_token(s_top[k][j]);
-        const float xv = logits[(int64_t)(b * K + k) * V + col];
-        cv[n] = ocum[k] + ((xv - s_mx[k]) - s_ls[k]);
-        cf[n++] = k * V + col;
-      }
-    }
-    for (int j = 0; j < K; ++j) {  // selection: best remaining (score desc, flat index asc)
-      int bi = -1;
-      for (int i = 0; i < n; ++i) {
-        if (cf[i] < 0) continue;
-        if (bi < 0 || cv[i] > cv[bi] || (cv[i] == cv[bi] && cf[i] < cf[bi])) bi = i;
-      }
-      const int pk = cf[bi] / V, col = cf[bi] % V, r = b * K + j;
-      cum[r] = cv[bi];
-      fin[r] = (ofin[pk] || col == end_id) ? 1 : 0;
-      tok[r] = col;
-      par[r] = b * K + pk;
-      htok[(int64_t)t * R + r] = col;
-      hpar[(int64_t)t * R + r] = pk;
-      cf[bi] = -1;
-    }
-  }
-}
-
 // One workgroup per image: trace every final beam back (seqs [B][K][T], scores [B][K]); ids, alpha
 // and beta follow beam 0.  path [B][T] scratch: the row whose step-t attention produced beam 0's
 // token t.
@@ -200,6 +106,66 @@ __device__ __forceinline__ void red_bfly(float (&v)[16], int li) {
     const float rv = __uint_as_float(partner<M>(__float_as_uint(sd)));
     v[k] = OP == 0 ? fmaxf(kp, rv) : kp + rv;
   }
+}
+
+// Granule summary of one 32 x 32 block held in MFMA accumulator layout (lane li + 32 lh holds
+// column li of rows acc_row(r, lane), r = 0..15): per row, (max, sum exp(x - max)) over the block's
+// 32 columns (invalid columns: x = -inf, no term), by a transposing max-butterfly, a broadcast of the
+// row max to the row's 32 lanes, one expf per element and a transposing add-butterfly -- a fixed
+// pattern, so every kernel that calls this on the same values gets the same bits (the beam-search
+// selection's log-sum-exp is built from these summaries).  Returns the summary in lanes with
+// !(li & 1), for the row of the block acc_row-indexed by sum_row().
+__device__ __forceinline__ float2 granule_summary(const float (&x)[16], bool valid, int li, int lh) {
+  float m[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) m[r] = x[r];
+  red_bfly<16, 0>(m, li);
+  red_bfly<8, 0>(m, li);
+  red_bfly<4, 0>(m, li);
+  red_bfly<2, 0>(m, li);
+  const float gmax = fmaxf(m[0], __uint_as_float(partner<1>(__float_as_uint(m[0]))));
+  // lane pair (2 rr, 2 rr + 1) of half lh now holds the max of row rr of that half
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float g = __shfl(gmax, 2 * r + 32 * lh, 64);
+    m[r] = valid ? expf(x[r] - g) : 0.f;
+  }
+  red_bfly<16, 1>(m, li);
+  red_bfly<8, 1>(m, li);
+  red_bfly<4, 1>(m, li);
+  red_bfly<2, 1>(m, li);
+  const float gs = m[0] + __uint_as_float(partner<1>(__float_as_uint(m[0])));
+  return make_float2(gmax, gs);
+}
+// block row of the summary granule_summary leaves in lane li (valid in lanes with !(li & 1))
+__device__ __forceinline__ int sum_row(int li, int lh) {
+  const int rr = (li >> 1) & 15;
+  return (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+}
+
+// Granule summaries of logits already in memory (the exact path: k_vocab's fp32 logits, row pitch
+// Vp): one wave per (32-row block, 32-column granule), the block loaded in accumulator layout and
+// summarised by granule_summary -- bit-identical to the summaries a GEMM epilogue computes from the
+// same logit values.
+__global__ __launch_bounds__(256) void k_gsumm(int R, int V, int Vp, const float* __restrict__ logits,
+                                               float2* __restrict__ gsum) {
+  const int NG = Vp / 32, RB = (R + 31) / 32;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave = (row block, granule)
+  if (gw >= RB * NG) return;
+  const int rb = gw / NG, g = gw % NG;
+  const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int col = g * 32 + li;
+  const bool valid = col < V;
+  float x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int row = rb * 32 + acc_row(r, lane);
+    row = row < R ? row : R - 1;
+    x[r] = valid ? logits[(int64_t)row * Vp + col] : -INFINITY;
+  }
+  const float2 sm = granule_summary(x, valid, li, lh);
+  const int row = rb * 32 + sum_row(li, lh);
+  if (!(li & 1) && row < R) gsum[(int64_t)row * NG + g] = sm;
 }
 
 // k_vbeam4: logits (+ bias) and per (row, 32-column granule) (max, sum exp(x - max)), bf16x3 MFMA
@@ -310,34 +276,17 @@ __global__ __launch_bounds__(256, 2) void k_vbeam4(int R, int V, int Vp, const b
     const float bv = bias[col];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      float x[16], m[16];
+      float x[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         x[r] = acc[a][c][r] + bv;
         const int row = m0 + wr * 64 + a * 32 + acc_row(r, lane);
         if (row < R) logits[(int64_t)row * Vp + col] = x[r];
         x[r] = valid ? x[r] : -INFINITY;
-        m[r] = x[r];
       }
-      red_bfly<16, 0>(m, li);
-      red_bfly<8, 0>(m, li);
-      red_bfly<4, 0>(m, li);
-      red_bfly<2, 0>(m, li);
-      const float gmax = fmaxf(m[0], __uint_as_float(partner<1>(__float_as_uint(m[0]))));
-      // lane pair (2 rr, 2 rr + 1) of half lh now holds the max of row rr of that half
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float g = __shfl(gmax, 2 * r + 32 * lh, 64);
-        m[r] = valid ? expf(x[r] - g) : 0.f;
-      }
-      red_bfly<16, 1>(m, li);
-      red_bfly<8, 1>(m, li);
-      red_bfly<4, 1>(m, li);
-      red_bfly<2, 1>(m, li);
-      const float gs = m[0] + __uint_as_float(partner<1>(__float_as_uint(m[0])));
-      const int rr = (li >> 1) & 15;
-      const int row = m0 + wr * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = make_float2(gmax, gs);
+      const float2 sm = granule_summary(x, valid, li, lh);
+      const int row = m0 + wr * 64 + a * 32 + sum_row(li, lh);
+      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = sm;
     }
   }
 }
@@ -424,33 +373,17 @@ __global__ __launch_bounds__(1024) void k_vbeam5(int R, int V, int Vp, const bf1
     const float bv = bias[col];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      float x[16], m[16];
+      float x[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         x[r] = acc[a][c][r] + bv;
         const int row = m0 + wr * 64 + a * 32 + acc_row(r, lane);
         if (row < R) logits[(int64_t)row * Vp + col] = x[r];
         x[r] = valid ? x[r] : -INFINITY;
-        m[r] = x[r];
       }
-      red_bfly<16, 0>(m, li);
-      red_bfly<8, 0>(m, li);
-      red_bfly<4, 0>(m, li);
-      red_bfly<2, 0>(m, li);
-      const float gmax = fmaxf(m[0], __uint_as_float(partner<1>(__float_as_uint(m[0]))));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float g = __shfl(gmax, 2 * r + 32 * lh, 64);
-        m[r] = valid ? expf(x[r] - g) : 0.f;
-      }
-      red_bfly<16, 1>(m, li);
-      red_bfly<8, 1>(m, li);
-      red_bfly<4, 1>(m, li);
-      red_bfly<2, 1>(m, li);
-      const float gs = m[0] + __uint_as_float(partner<1>(__float_as_uint(m[0])));
-      const int rr = (li >> 1) & 15;
-      const int row = m0 + wr * 64 + a * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = make_float2(gmax, gs);
+      const float2 sm = granule_summary(x, valid, li, lh);
+      const int row = m0 + wr * 64 + a * 32 + sum_row(li, lh);
+      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + (n0 + wc * 64 + c * 32) / 32] = sm;
     }
   }
 }
@@ -659,7 +592,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
   hipStream_t s = (hipStream_t)stream;
   const MP p = resolve(m, L);
   const int H = L.H, R = B * K;
-  const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
+  const bool exact = (flags & AA_BEAM_FAST) == 0;  // default: exact fp32 logits
   // encoder tail for the B images; h0 / c0 / x_g expanded to the R = B*K rows
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[1], w.c[1], w.vwv, w.xg1, nullptr, 0, s);
   if (rc) return rc;
@@ -682,10 +615,13 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
                       w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
                       w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K, exact ? nullptr : w.u3);
     if (exact) {
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, w.u, p.mlp_w, p.mlp_b,
-                         w.logits, (uint64_t*)nullptr);
-      hipLaunchKernelGGL(k_beam_select, dim3(B), dim3(256), 0, s, K, L.V, R, t, end_id < 0 ? -1 : end_id, w.logits,
-                         w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
+      // exact fp32 logits (k_vocab's fma chains, pitch Vp), their granule summaries, selection
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, L.Vp, w.u, p.mlp_w,
+                         p.mlp_b, w.logits, (uint64_t*)nullptr);
+      hipLaunchKernelGGL(k_gsumm, dim3((unsigned)((((R + 31) / 32) * (L.Vp / 32) + 3) / 4)), dim3(256), 0, s, R, L.V,
+                         L.Vp, w.logits, w.gsum);
+      hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
+                         w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {
 #define AA_VB3(H_)                                                                                            \
   if (wide)                                                                                                   \

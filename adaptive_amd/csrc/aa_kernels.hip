@@ -2051,7 +2051,7 @@ __global__ __launch_bounds__(256) void k_logits_at(int H, int V, const float* __
 // argmax of sampler (:201) fused into the epilogue: per-row max over the tile's columns by 64-bit
 // keys (lane shuffles, then LDS across the two column waves), one atomicMax per row per workgroup.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, const float* __restrict__ u,
+__global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, int ld, const float* __restrict__ u,
                                                const float* __restrict__ W, const float* __restrict__ bias,
                                                float* __restrict__ scores, uint64_t* __restrict__ keys) {
   constexpr int BM = 64, BN = 64;
@@ -2074,7 +2074,7 @@ __global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, cons
     const float p45 = acc[4][0][0][r] + acc[5][0][0][r], p67 = acc[6][0][0][r] + acc[7][0][0][r];
     const float x = ((p01 + p23) + (p45 + p67)) + bv;
     const int row = mt * BM + wm * 32 + acc_row(r, lane);
-    if (scores && valid && row < B) scores[(int64_t)row * V + col] = x;
+    if (scores && valid && row < B) scores[(int64_t)row * ld + col] = x;
     uint64_t k = valid ? argmax_key(x, col) : 0ull;
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
@@ -2642,7 +2642,7 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   }
   lstm_atten_launch(L, p, B, tok, 1, V, VWv, w.xg, w.hsp, c_in, h_out, nullptr, c_out, w.s, w.part, w.u,
                     nullptr, nullptr, alpha, P, beta, 1, nullptr, 0, s);
-  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, p.mlp_w,
+  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V, w.u, p.mlp_w,
                      p.mlp_b, scores, w.keys);
   hipLaunchKernelGGL(k_finalize, dim3((B + 255) / 256), dim3(256), 0, s, w.keys, B, 1, tokens_out);
   return launch_status();
@@ -2726,7 +2726,7 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     rec(sev, 2 * t, s);
     if (exact) {
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, p.mlp_w, p.mlp_b,
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, L.V, u, p.mlp_w, p.mlp_b,
                          nullptr, kt);
       rec(sev, 2 * t + 1, s);
       hipLaunchKernelGGL(k_key_ids, dim3((Bl + 255) / 256), dim3(256), 0, s, kt, Bl, idsl + t, T);
@@ -2946,7 +2946,7 @@ int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* scores,
   if (!u || !scores) return AA_ERR_NULL;
   if (!al16(u)) return AA_ERR_ALIGN;
   const MP p = resolve(m, L);
-  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, (hipStream_t)stream, B, L.H, L.V, L.Vp,
+  hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, (hipStream_t)stream, B, L.H, L.V, L.Vp, L.V,
                      u, p.mlp_w, p.mlp_b, scores, nullptr);
   return launch_status();
 }

@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tile128", action="store_true", help="vocab logits on 128x128 tiles (k_vbeam4) instead of "
                     "256x256 (k_vbeam5)")
+    ap.add_argument("--fast", action="store_true", help="opt-in bf16x3 logits (AA_BEAM_FAST) instead of the exact "
+                    "fp32 default")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, K, T = args.batch, args.beam, args.T
@@ -66,11 +68,11 @@ def main():
     model.beam_tile128 = args.tile128
     feats = synthetic_features(B, dev, seed=0)
     for _ in range(args.warmup):
-        model.beam_search(feats, T, K)
+        model.beam_search(feats, T, K, fast=args.fast)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = model.beam_search(feats, T, K)
+        out = model.beam_search(feats, T, K, fast=args.fast)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     res = {"metric": f"captions/sec (beam {K}, max_len={T}) at B={B}", "value": B * args.steps / el,
@@ -79,7 +81,9 @@ def main():
            "data": "synthetic: U[0,1) post-trunk features, random-init weights (adaptive_amd.synth seed 123)",
            "config": {"workload": f"Encoder2Decoder.beam_search B={B} beam={K} max_len={T}", "batch": B,
                       "beam": K, "T": T, "rows": B * K,
-                      "vocab_kernel": "k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"},
+                      "vocab_kernel": ("bf16x3 " + ("k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"))
+                      if args.fast else "exact fp32: k_vocab (fp32 MFMA) + k_gsumm summaries",
+                      "mode": "fast (opt-in bf16x3)" if args.fast else "exact (default)"},
            "best_score_mean": float(out[4][:, 0].mean().item()), "cpu_baseline": None}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(K, T, args.cpu_sample, args.cpu_budget)

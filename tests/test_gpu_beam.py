@@ -1,5 +1,6 @@
 """Beam-search decode (BASELINE config 4) on the GPU through the C-ABI
-(aa_beam_decode) against oracle/adaptive_oracle.py BeamOracle.
+(aa_beam_decode) against oracle/adaptive_oracle.py BeamOracle.  The default path computes exact
+fp32 logits (the greedy exact mode's GEMM); ``fast=True`` is the opt-in bf16x3 mode.
 
 The reference has no beam search (for_wzn:3 is a TODO), so BeamOracle — the reference's own
 decoder step under build-defined selection rules — is the specification: parity unpinned by the
@@ -37,17 +38,17 @@ def _model(dev, sd):
     return m
 
 
-@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("boost,B,T,K,fseed", [(0.0, 4, 20, 3, 0), (2.6, 8, 12, 3, 0), (2.8, 5, 10, 5, 3),
                                                (0.0, 3, 8, 8, 1)])
-def test_beam_vs_oracle(boost, B, T, K, fseed, exact, gpu_device):
+def test_beam_vs_oracle(boost, B, T, K, fseed, fast, gpu_device):
     sd = _weights(end_boost=boost)
     feats = synth.make_features(B, seed=fseed)
     o_ids, o_al, o_be, o_seqs, o_sc, margin = BeamOracle(sd).beam_search(torch.from_numpy(feats), T, K,
                                                                          return_margin=True)
     assert margin > 4 * SCORE_TOL, f"oracle case too close to call: margin {margin}"
     ids, al, be, seqs, sc = _model(gpu_device, sd).beam_search(torch.from_numpy(feats).to(gpu_device), T, K,
-                                                                exact_vocab=exact)
+                                                                fast=fast)
     assert torch.equal(seqs.cpu(), o_seqs)
     assert torch.equal(ids.cpu(), o_ids)
     np.testing.assert_allclose(sc.cpu().numpy(), o_sc.numpy(), atol=SCORE_TOL, rtol=0)
@@ -57,44 +58,66 @@ def test_beam_vs_oracle(boost, B, T, K, fseed, exact, gpu_device):
         assert (o_seqs == 2).any(), "case meant to exercise finished beams has none"
 
 
-@pytest.mark.parametrize("exact", [False, True])
-def test_beam1_equals_greedy(exact, gpu_device):
+@pytest.mark.parametrize("fast", [False, True])
+def test_beam1_equals_greedy(fast, gpu_device):
     """K = 1 without an end token is the greedy decode (candidate order = logit order): bit-exact
-    with the fp32 logits; with the bf16x3 logits the ids agree wherever the greedy top-2 margin
-    exceeds the bf16x3-vs-fp32 difference (every row of this batch)."""
+    with the exact fp32 logits (two implementations: k_vocab + granule summaries + selection against
+    the greedy screen + exact rescoring); with the bf16x3 logits the ids agree wherever the greedy
+    top-2 margin exceeds the bf16x3-vs-fp32 difference (every row of this batch)."""
     m = _model(gpu_device, _weights())
     feats = synth.make_features(64, seed=2)
     f = torch.from_numpy(feats).to(gpu_device)
     g_ids, g_al, g_be = m.sampler(f, max_len=20)
-    ids, al, be, seqs, sc = m.beam_search(f, 20, 1, end_id=-1, exact_vocab=exact)
+    ids, al, be, seqs, sc = m.beam_search(f, 20, 1, end_id=-1, fast=fast)
     assert torch.equal(ids, g_ids)
     assert torch.equal(seqs[:, 0], g_ids)
     torch.testing.assert_close(al, g_al, atol=0, rtol=0)
     torch.testing.assert_close(be, g_be, atol=0, rtol=0)
 
 
-def test_beam_bf16x3_logits_match_fp32(gpu_device):
-    """Default (bf16x3 + fused summaries) and exact-vocab (fp32 GEMM) beams agree at config-4 shape
-    wherever the selection margins allow: same sequences for all but a handful of images, scores
-    within SCORE_TOL where the sequences agree."""
+def test_beam_fast_mode_agreement(gpu_device):
+    """The opt-in bf16x3 mode against the exact default at config-4 shape: the same beams except
+    where two candidates are within the logits' rounding difference (an approximate mode, so only
+    its agreement rate is asserted: >= 98% of images), scores within SCORE_TOL where equal."""
     m = _model(gpu_device, _weights(end_boost=2.6))
     f = torch.from_numpy(synth.make_features(512, seed=6)).to(gpu_device)
-    a = m.beam_search(f, 20, 3)
-    b = m.beam_search(f, 20, 3, exact_vocab=True)
+    a = m.beam_search(f, 20, 3, fast=True)
+    b = m.beam_search(f, 20, 3)
     same = (a[3] == b[3]).flatten(1).all(1)
     assert same.float().mean().item() > 0.98
     torch.testing.assert_close(a[4][same], b[4][same], atol=SCORE_TOL, rtol=0)
 
 
+def test_beam_config4_b512_equals_oracle_on_64_images(gpu_device):
+    """Config 4 at its size (B = 512, K = 3, T = 20, exact default): images 0..63 of the batch equal
+    BeamOracle (sequences bitwise, scores within SCORE_TOL, alpha / beta within ATT_TOL).  The data's
+    smallest selection gap over those 64 images x 20 steps (2.6e-5, measured on the oracle) is
+    asserted first: it is a property of this pinned input, far above the ~1e-6 fp32 differences
+    between the GPU and CPU scores, so the sequence comparison below is unconditional."""
+    K, T = 3, 20
+    sd = _weights()
+    m = _model(gpu_device, sd)
+    feats = synth.make_features(512, seed=0)
+    ids, al, be, seqs, sc = m.beam_search(torch.from_numpy(feats).to(gpu_device), T, K)
+    o_ids, o_al, o_be, o_seqs, o_sc, margin = BeamOracle(sd).beam_search(torch.from_numpy(feats[:64]), T, K,
+                                                                         return_margin=True)
+    assert margin > 1e-5, f"pinned input changed: selection margin {margin}"
+    assert torch.equal(seqs[:64].cpu(), o_seqs)
+    assert torch.equal(ids[:64].cpu(), o_ids)
+    np.testing.assert_allclose(sc[:64].cpu().numpy(), o_sc.numpy(), atol=SCORE_TOL, rtol=0)
+    np.testing.assert_allclose(al[:64].cpu().numpy(), o_al.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(be[:64].cpu().numpy(), o_be.numpy(), atol=ATT_TOL, rtol=0)
+
+
 def test_beam_tile256_equals_tile128(gpu_device):
-    """k_vbeam5 (256 x 256 tiles, the default when the padded vocabulary is whole 256-column tiles)
-    and k_vbeam4 (128 x 128) run the same per-element product order: bit-identical beams."""
+    """Fast mode: k_vbeam5 (256 x 256 tiles, used when the padded vocabulary is whole 256-column
+    tiles) and k_vbeam4 (128 x 128) run the same per-element product order: bit-identical beams."""
     m = _model(gpu_device, _weights(end_boost=2.6))
     f = torch.from_numpy(synth.make_features(200, seed=8)).to(gpu_device)
-    a = m.beam_search(f, 12, 3)
+    a = m.beam_search(f, 12, 3, fast=True)
     m.beam_tile128 = True
     try:
-        b = m.beam_search(f, 12, 3)
+        b = m.beam_search(f, 12, 3, fast=True)
     finally:
         m.beam_tile128 = False
     for x, y in zip(a, b):
@@ -112,8 +135,8 @@ def test_beam_batch_invariance(gpu_device):
 
 
 def test_beam_b512_properties(gpu_device):
-    """Config 4 shape (B = 512, K = 3, T = 20): beams sorted, ids = best beam, finished beams stay
-    finished, the first images agree with the oracle."""
+    """Config 4 shape (B = 512, K = 3, T = 20) with <end> made competitive: beams sorted, ids = best
+    beam, finished beams stay finished (oracle parity at this size: the 64-image test above)."""
     K, T = 3, 20
     sd = _weights(end_boost=2.6)
     m = _model(gpu_device, sd)
@@ -126,10 +149,7 @@ def test_beam_b512_properties(gpu_device):
     ended = (seqs_c == 2).int().cummax(dim=2).values.bool()
     assert torch.all(seqs_c[ended] == 2)
     assert torch.allclose(al.sum(-1).cpu(), torch.ones(512, T), atol=1e-5)
-    o = BeamOracle(sd).beam_search(torch.from_numpy(feats[:6]), T, K, return_margin=True)
-    if o[5] > 4 * SCORE_TOL:
-        assert torch.equal(seqs_c[:6], o[3])
-        np.testing.assert_allclose(sc_c[:6].numpy(), o[4].numpy(), atol=SCORE_TOL, rtol=0)
+    assert ended.any(), "case meant to exercise finished beams has none"
 
 
 def test_beam_errors_are_loud(gpu_device):
