@@ -435,13 +435,16 @@ class Encoder2Decoder(nn.Module):
         beam best first with its cumulative log-probability.  ``end_id`` = the vocabulary's
         ``<end>`` (2 in build_vocab.py's order); a beam that emits it is finished; -1 disables.
         Logits are exact fp32 (the fp32 MFMA GEMM's fma chains, as the greedy path's exact mode) by
-        default; ``fast=True`` (or the older ``exact_vocab=False``) computes them by bf16x3 MFMA with
-        fused log-sum-exp summaries -- fp32-accurate but not bitwise, so a near-tie between two
-        candidates can be decided differently (opt-in speed mode)."""
+        default, in one fused launch per step (k_vexact); ``exact_vocab=True`` runs the same arithmetic
+        as two launches (the plain fp32 GEMM k_vocab, then k_gsumm) -- the cross-check, bitwise equal;
+        ``fast=True`` (or ``exact_vocab=False``) computes the logits by bf16x3 MFMA with fused
+        log-sum-exp summaries -- fp32-accurate but not bitwise, so a near-tie between two candidates
+        can be decided differently (opt-in speed mode)."""
+        check = False
         if exact_vocab is not None:
             if exact_vocab and fast:
                 raise ValueError("exact_vocab=True contradicts fast=True")
-            fast = not exact_vocab
+            fast, check = not exact_vocab, bool(exact_vocab)
         images = self._check_images(self.features(images))
         model = self._model_struct()
         lib = _lib.load()
@@ -461,7 +464,7 @@ class Encoder2Decoder(nn.Module):
             rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
                                     ws.numel() if ws is not None else 0,
-                                    (_lib.BEAM_FAST if fast else 0)
+                                    (_lib.BEAM_FAST if fast else 0) | (_lib.DECODE_EXACT_VOCAB if check else 0)
                                     | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle())
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores

@@ -168,6 +168,49 @@ __global__ __launch_bounds__(256) void k_gsumm(int R, int V, int Vp, const float
   if (!(li & 1) && row < R) gsum[(int64_t)row * NG + g] = sm;
 }
 
+// k_vexact (the beam's default vocab stage): exact fp32 logits -- k_vocab's arithmetic (the same
+// v_mfma_f32_32x32x2f32 sequence over NP_VOCAB chains and the same combination tree, via
+// gemm_mainloop_chain), so the same bits -- on 128 x 64 tiles (each wave 64 x 32: two blocks, where
+// k_vocab's 64 x 64 tiles give each wave one block and hold all 8 chains), with the granule summaries
+// of k_gsumm fused into the epilogue (granule_summary on the same values: the same bits).
+// k_vocab + k_gsumm stay as the cross-check path (AA_DECODE_EXACT_VOCAB).
+constexpr int VX_BM = 128, VX_BN = 64;
+__global__ __launch_bounds__(256, 1) void k_vexact(int R, int H, int V, int Vp, const float* __restrict__ u,
+                                                   const float* __restrict__ W, const float* __restrict__ bias,
+                                                   float* __restrict__ logits, float2* __restrict__ gsum) {
+  __shared__ __attribute__((aligned(16))) float lds[Tile<VX_BM, VX_BN>::LDS_FLOATS];
+  const int MT = (R + VX_BM - 1) / VX_BM, NTn = Vp / VX_BN, NG = Vp / 32;
+  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  ARowMajor al{u, H, mt * VX_BM, R};
+  WRowMajor wl{W, H, nt * VX_BN};
+  floatx16 acc[VX_BM / 64][VX_BN / 64];
+  gemm_mainloop_chain<VX_BM, VX_BN, NP_VOCAB>(al, wl, H / BK, lds, acc);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tn = 0; tn < VX_BN / 64; ++tn) {
+    const int c0 = nt * VX_BN + wn * (VX_BN / 2) + tn * 32, col = c0 + li;
+    const bool valid = col < V;
+    const float bv = bias[col];
+#pragma unroll
+    for (int tm = 0; tm < VX_BM / 64; ++tm) {
+      const int rb = mt * VX_BM + wm * (VX_BM / 2) + tm * 32;
+      float x[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[r] = acc[tm][tn][r] + bv;
+        const int row = rb + acc_row(r, lane);
+        if (row < R) logits[(int64_t)row * Vp + col] = x[r];
+        x[r] = valid ? x[r] : -INFINITY;
+      }
+      const float2 sm = granule_summary(x, valid, li, lh);
+      const int row = rb + sum_row(li, lh);
+      if (!(li & 1) && row < R) gsum[(int64_t)row * NG + c0 / 32] = sm;
+    }
+  }
+}
+
 // k_vbeam4: logits (+ bias) and per (row, 32-column granule) (max, sum exp(x - max)), bf16x3 MFMA
 // (fp32-accurate, as the encoder / LSTM GEMMs), from a 128x128 tile whose operand fragments
 // are staged once per workgroup in LDS by global_load_lds (16 B per lane: one wave instruction
@@ -615,11 +658,17 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
                       w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
                       w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K, exact ? nullptr : w.u3);
     if (exact) {
-      // exact fp32 logits (k_vocab's fma chains, pitch Vp), their granule summaries, selection
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, L.Vp, w.u, p.mlp_w,
-                         p.mlp_b, w.logits, (uint64_t*)nullptr);
-      hipLaunchKernelGGL(k_gsumm, dim3((unsigned)((((R + 31) / 32) * (L.Vp / 32) + 3) / 4)), dim3(256), 0, s, R, L.V,
-                         L.Vp, w.logits, w.gsum);
+      // exact fp32 logits (k_vocab's fma chains, pitch Vp) and their granule summaries: one fused
+      // launch (k_vexact), or -- AA_DECODE_EXACT_VOCAB, the cross-check -- k_vocab then k_gsumm
+      if (flags & AA_DECODE_EXACT_VOCAB) {
+        hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, R, H, L.V, L.Vp, L.Vp, w.u, p.mlp_w,
+                           p.mlp_b, w.logits, (uint64_t*)nullptr);
+        hipLaunchKernelGGL(k_gsumm, dim3((unsigned)((((R + 31) / 32) * (L.Vp / 32) + 3) / 4)), dim3(256), 0, s, R,
+                           L.V, L.Vp, w.logits, w.gsum);
+      } else {
+        hipLaunchKernelGGL(k_vexact, dim3(((R + VX_BM - 1) / VX_BM) * (L.Vp / VX_BN)), dim3(256), 0, s, R, H, L.V,
+                           L.Vp, w.u, p.mlp_w, p.mlp_b, w.logits, w.gsum);
+      }
       hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
                          w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {

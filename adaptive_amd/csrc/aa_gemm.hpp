@@ -232,4 +232,108 @@ __device__ __forceinline__ void gemm_mainloop_np(const AL& al, const WL& wl, int
   }
 }
 
+// gemm_mainloop_np's arithmetic (NP chains over contiguous K ranges, each the same MFMA sequence)
+// with the chains combined as they complete, in the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7))
+// (NP = 8; a binary-counter reduction, so at most log2(NP) + 1 partial sets are live instead of NP):
+// out is bit-identical to that tree over gemm_mainloop_np's partials, at a quarter of its
+// accumulator registers for NP = 8 -- room for several 32 x 32 blocks per wave.
+template <int BM, int BN, int NP, class AL, class WL>
+__device__ __forceinline__ void gemm_mainloop_chain(const AL& al, const WL& wl, int nk, float* lds,
+                                                    floatx16 (&out)[BM / 64][BN / 64]) {
+  using T = Tile<BM, BN>;
+  static_assert(NP == 8, "the combination tree below is written for 8 chains");
+  constexpr int TM = T::TM, TN = T::TN;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  floatx16 cur[TM][TN], h0[TM][TN], h1[TM][TN], h2[TM][TN];
+  float4 ra[T::AF4], rw[T::WF4];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < T::AF4; ++i) ra[i] = al.load(i, t + NT * i, ks * BK);
+#pragma unroll
+    for (int i = 0; i < T::WF4; ++i) rw[i] = wl.load(t + NT * i, ks * BK);
+  };
+  auto lstore = [&](int buf) {
+    float* As = lds + buf * T::STAGE;
+    float* Ws = As + BM * LDK;
+#pragma unroll
+    for (int i = 0; i < T::AF4; ++i) {
+      int r, kq;
+      al.map(t + NT * i, r, kq);
+      *reinterpret_cast<float4*>(As + r * LDK + 4 * kq) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < T::WF4; ++i) {
+      const int q = t + NT * i;
+      *reinterpret_cast<float4*>(Ws + (q >> 3) * LDK + 4 * (q & 7)) = rw[i];
+    }
+  };
+  auto add = [](floatx16 (&d)[TM][TN], const floatx16 (&a)[TM][TN], const floatx16 (&b)[TM][TN]) {
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[tm][tn][r] = a[tm][tn][r] + b[tm][tn][r];
+  };
+  const int per = nk / NP;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[tm][tn][r] = 0.f;
+    for (int k2 = 0; k2 < per; ++k2) {
+      const int ks = p * per + k2;
+      const int buf = ks & 1;
+      const bool more = ks + 1 < nk;
+      if (more) gload(ks + 1);
+      const float* As = lds + buf * T::STAGE;
+      const float* Ws = As + BM * LDK;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        float4 a[TM], w[TN];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+          a[tm] = *reinterpret_cast<const float4*>(As + (wm * (BM / 2) + tm * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          w[tn] = *reinterpret_cast<const float4*>(Ws + (wn * (BN / 2) + tn * 32 + li) * LDK + 16 * lh + 4 * s4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+              cur[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a[tm], j), f4c(w[tn], j), cur[tm][tn], 0, 0, 0);
+      }
+      if (more) lstore(buf ^ 1);
+      __syncthreads();
+    }
+    // binary-counter combination: p0 -> h0; p1 -> h1 = h0 + p1; p2 -> h0; p3 -> h2 = h1 + (h0 + p3);
+    // p4 -> h0; p5 -> h1 = h0 + p5; p6 -> h0; p7 -> out = h2 + (h1 + (h0 + p7))
+    if (p == 0 || p == 2 || p == 4 || p == 6) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) h0[tm][tn] = cur[tm][tn];
+    } else if (p == 1 || p == 5) {
+      add(h1, h0, cur);
+    } else if (p == 3) {
+      add(cur, h0, cur);
+      add(h2, h1, cur);
+    } else {  // p == 7
+      add(cur, h0, cur);
+      add(cur, h1, cur);
+      add(out, h2, cur);
+    }
+  }
+}
+
 }  // namespace aa

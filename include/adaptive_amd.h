@@ -292,13 +292,14 @@ AA_API int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, cons
  * the K best candidates per image (score desc, ties to the smaller parent*V + token) survive.
  * All T steps run.  Outputs (each may be NULL): ids [B,T] int64, alpha [B,T,P], beta [B,T] of the
  * best final beam; seqs [B,K,T] int64 and scores [B,K] of all K final beams, best first.
- * Logits (default): exact fp32 -- the fp32 MFMA GEMM of aa_vocab_logits (the same fma chains, so the
- * same bits) -- then per-32-column (max, sum exp(x - max)) summaries in a fixed butterfly order, from
- * which the selection builds each row's log-sum-exp.  flags & AA_BEAM_FAST: the logits by bf16x3
+ * Logits (default): exact fp32 -- the fma chains of aa_vocab_logits' fp32 MFMA GEMM, so the same
+ * bits -- with per-32-column (max, sum exp(x - max)) summaries in a fixed butterfly order fused into
+ * the GEMM epilogue (one launch per step); the selection builds each row's log-sum-exp from them.
+ * flags & AA_DECODE_EXACT_VOCAB: the same values by two launches (the plain fp32 GEMM, then the
+ * summaries) -- the cross-check path, bitwise equal to the default.  flags & AA_BEAM_FAST: the logits by bf16x3
  * MFMA (fp32-accurate but rounded differently) with the summaries fused into the GEMM epilogue --
  * about 2.3x faster, and the beams equal the exact ones except where two candidates are within the
  * logits' rounding difference of each other (measured: >= 98% of images at config 4).
- * AA_DECODE_EXACT_VOCAB is accepted and means the default.
  * Requires vocab <= 16384.  Replaces, for beam decoding, the greedy sampler's role in coco_eval
  * (code_src/tools/utils.py:171). */
 #define AA_MAX_BEAM 8

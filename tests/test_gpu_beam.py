@@ -76,7 +76,7 @@ def test_beam1_equals_greedy(fast, gpu_device):
 
 
 def test_beam_fast_mode_agreement(gpu_device):
-    """The opt-in bf16x3 mode against the exact default at config-4 shape: the same beams except
+    """The opt-in bf16x3 mode against the exact default at config-4 size: the same beams except
     where two candidates are within the logits' rounding difference (an approximate mode, so only
     its agreement rate is asserted: >= 98% of images), scores within SCORE_TOL where equal."""
     m = _model(gpu_device, _weights(end_boost=2.6))
@@ -86,6 +86,20 @@ def test_beam_fast_mode_agreement(gpu_device):
     same = (a[3] == b[3]).flatten(1).all(1)
     assert same.float().mean().item() > 0.98
     torch.testing.assert_close(a[4][same], b[4][same], atol=SCORE_TOL, rtol=0)
+
+
+def test_beam_config4_fused_exact_equals_two_launch_exact(gpu_device):
+    """Config 4 at its size (B = 512, K = 3, T = 20, <end> made competitive): the default fused exact
+    kernel (k_vexact: chained fp32 MFMA on 128 x 64 tiles + summaries in the epilogue) and the
+    cross-check path (k_vocab's plain fp32 GEMM, then k_gsumm) produce bitwise the same beams, scores,
+    alpha and beta -- two implementations of one arithmetic, no tolerance."""
+    m = _model(gpu_device, _weights(end_boost=2.6))
+    f = torch.from_numpy(synth.make_features(512, seed=6)).to(gpu_device)
+    a = m.beam_search(f, 20, 3)
+    b = m.beam_search(f, 20, 3, exact_vocab=True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert (a[3] == 2).any()  # finished beams occur in this case
 
 
 def test_beam_config4_b512_equals_oracle_on_64_images(gpu_device):
