@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 # AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
 LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libadaptive_amd.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
@@ -113,7 +113,7 @@ SIGNATURES = {
                                    c_void_p, c_size_t, c_int32, c_void_p]),
     "aa_beam_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32, c_int32]),
     "aa_beam_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
-                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p]),
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p, c_void_p]),
     "aa_vocab_logits": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_void_p]),
     "aa_vocab_logits_at": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),

@@ -428,7 +428,7 @@ class Encoder2Decoder(nn.Module):
 
     @torch.no_grad()
     def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2,
-                    exact_vocab: Optional[bool] = None, fast: bool = False):
+                    exact_vocab: Optional[bool] = None, fast: bool = False, vocab_events=None):
         """Beam-search decode (BASELINE config 4; not in the reference, semantics in
         include/adaptive_amd.h and DESIGN.md) -> (ids [B,T], alpha [B,T,49], beta [B,T,1],
         seqs [B,K,T], scores [B,K]): ids / alpha / beta of the best final beam, then every final
@@ -439,7 +439,9 @@ class Encoder2Decoder(nn.Module):
         as two launches (the plain fp32 GEMM k_vocab, then k_gsumm) -- the cross-check, bitwise equal;
         ``fast=True`` (or ``exact_vocab=False``) computes the logits by bf16x3 MFMA with fused
         log-sum-exp summaries -- fp32-accurate but not bitwise, so a near-tie between two candidates
-        can be decided differently (opt-in speed mode)."""
+        can be decided differently (opt-in speed mode).  ``vocab_events``: address of 2 * max_len raw
+        hipEvent handles (adaptive_amd.hip_events.EventArray.ptr) recorded around each step's vocab
+        stage, for per-launch timing."""
         check = False
         if exact_vocab is not None:
             if exact_vocab and fast:
@@ -465,7 +467,8 @@ class Encoder2Decoder(nn.Module):
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
                                     ws.numel() if ws is not None else 0,
                                     (_lib.BEAM_FAST if fast else 0) | (_lib.DECODE_EXACT_VOCAB if check else 0)
-                                    | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle())
+                                    | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle(),
+                                    vocab_events)
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores
 

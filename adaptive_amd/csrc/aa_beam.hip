@@ -619,7 +619,7 @@ size_t aa_beam_workspace_bytes(const aa_dims* d, int32_t B, int32_t T, int32_t K
 
 int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K, int32_t end_id,
                    int64_t* ids, int64_t* seqs, float* scores, float* alpha, float* beta, void* workspace,
-                   size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
+                   size_t workspace_bytes, int32_t flags, aa_stream_t stream, aa_event_t* vocab_events) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
@@ -657,6 +657,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
     lstm_atten_launch(L, p, R, t ? w.tok : w.tok0, 1, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt],
                       w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
                       w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K, exact ? nullptr : w.u3);
+    rec(vocab_events, 2 * t, s);
     if (exact) {
       // exact fp32 logits (k_vocab's fma chains, pitch Vp) and their granule summaries: one fused
       // launch (k_vexact), or -- AA_DECODE_EXACT_VOCAB, the cross-check -- k_vocab then k_gsumm
@@ -669,6 +670,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
         hipLaunchKernelGGL(k_vexact, dim3(((R + VX_BM - 1) / VX_BM) * (L.Vp / VX_BN)), dim3(256), 0, s, R, H, L.V,
                            L.Vp, w.u, p.mlp_w, p.mlp_b, w.logits, w.gsum);
       }
+      rec(vocab_events, 2 * t + 1, s);
       hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
                          w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {
@@ -688,6 +690,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
         default: AA_VB3(1024); break;
       }
 #undef AA_VB3
+      rec(vocab_events, 2 * t + 1, s);
       hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
                          w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     }

@@ -25,6 +25,10 @@ sys.path.insert(0, ROOT)
 
 from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
 from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
+from adaptive_amd.hip_events import EventArray  # noqa: E402
+
+PEAK_FP32 = 157.3e12       # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+PEAK_X3 = 2.5e15 / 6       # fp32-accurate bf16x3 GEMM: six bf16 MFMA products per fp32 product
 
 
 def cpu_baseline(K, T, sample, budget_s):
@@ -75,6 +79,31 @@ def main():
         out = model.beam_search(feats, T, K, fast=args.fast)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # traced pass (the same calls again): HIP events on the launch stream around every step's vocab
+    # stage -- the dominant kernel (k_vexact: exact fp32 logits + granule summaries; fast mode:
+    # k_vbeam5 / k_vbeam4) -- for its average launch duration
+    evs = [EventArray(2 * T) for _ in range(args.steps)]
+    for ev in evs:
+        model.beam_search(feats, T, K, fast=args.fast, vocab_events=ev.ptr)
+    torch.cuda.synchronize()
+    durs = [d for ev in evs for d in ev.pair_durations_ms()]
+    avg_ms = float(np.mean(durs))
+    Vn, H = model.dims.vocab, model.dims.hidden
+    flops = 2.0 * B * K * Vn * H  # algorithmic: the [B K, H] x [H, V] logits GEMM of one step
+    peak = PEAK_X3 if args.fast else PEAK_FP32
+    kname = ("k_vbeam4" if args.tile128 else "k_vbeam5") if args.fast else "k_vexact"
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic_beam.json")) as f:
+            traffic = json.load(f).get(kname, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    roofline = {"kernel": kname, "bound": "mfma", "achieved": flops / (avg_ms * 1e-3) / 1e12, "peak": peak / 1e12,
+                "unit": "TFLOP/s", "frac": flops / (avg_ms * 1e-3) / peak, "traffic": traffic,
+                "avg_launch_ms": avg_ms, "launches_timed": len(durs), "algorithmic_flops_per_launch": flops,
+                "note": ("bf16x3 GEMM priced at bf16 peak / 6" if args.fast else
+                         "exact fp32 GEMM on v_mfma_f32_32x32x2f32, priced at the fp32 MFMA peak") +
+                        "; the launch also writes the per-granule (max, sum exp) summaries"}
     res = {"metric": f"captions/sec (beam {K}, max_len={T}) at B={B}", "value": B * args.steps / el,
            "unit": "captions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "dtype": "fp32",
@@ -84,7 +113,7 @@ def main():
                       "vocab_kernel": ("bf16x3 " + ("k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"))
                       if args.fast else "exact fp32: k_vocab (fp32 MFMA) + k_gsumm summaries",
                       "mode": "fast (opt-in bf16x3)" if args.fast else "exact (default)"},
-           "best_score_mean": float(out[4][:, 0].mean().item()), "cpu_baseline": None}
+           "best_score_mean": float(out[4][:, 0].mean().item()), "roofline": roofline, "cpu_baseline": None}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(K, T, args.cpu_sample, args.cpu_budget)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]

@@ -41,6 +41,26 @@ def make_batch(B, T, seed=0):
     return caps, lengths
 
 
+PEAK_BF16 = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32 = 157.3e12
+
+
+def train_flops(B, T, lengths, E=256, H=512, V=10123, C=2048, P=49):
+    """Algorithmic GEMM FLOPs of one training step (forward + backward): every GEMM's
+    forward product, its weight gradient and -- except the encoder's, whose input (the post-trunk
+    features) needs no gradient here -- its input gradient.  Elementwise work, softmaxes, the
+    attention's 49 x 49 terms and Adam are not counted."""
+    R, N = B * T, int(sum(lengths))
+    g = {  # name: (M, N_out, K) of the forward product
+        "enc_V": (B * P, H, C), "enc_heads": (B, E + 2 * H, C), "VWv": (B * P, P, H),
+        "x_terms": (R, 5 * H, 2 * E), "lstm_hh": (R, 4 * H, H), "sentinel_h": (R - B, H, H),
+        "att_proj": (R, 2 * P, H), "vocab": (N, V, H)}
+    fwd = sum(2 * m * n * k for m, n, k in g.values())
+    bwd = sum(2 * 2 * m * n * k for m, n, k in g.values()) - 2 * B * P * H * C  # no d(features)
+    ctx = 2 * R * P * H  # context sum_k alpha_k V_k (forward), counted once
+    return {"total": fwd + bwd + ctx, "forward": fwd + ctx, "backward": bwd, "gemms": g}
+
+
 def step(model, opt, feats, caps, lengths):
     model.zero_grad()
     opt.zero_grad()
@@ -113,6 +133,15 @@ def main():
                       "gemm": "bf16 operands, fp32 accumulate (v_mfma_f32_32x32x16_bf16), fp32 master weights / Adam"
                       if args.dtype == "bf16" else "fp32 (v_mfma_f32_32x32x2f32)"},
            "final_loss": float(loss.item()), "cpu_baseline": None}
+    fl = train_flops(B, T, lengths)
+    peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_FP32
+    achieved = fl["total"] / (el / args.steps)
+    out["roofline"] = {"kernel": "whole step (k_tgemm GEMMs + elementwise + Adam)", "bound": "mfma",
+                       "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
+                       "traffic": None, "flops_per_step": fl["total"],
+                       "note": "algorithmic GEMM FLOPs of forward + backward (bench_train.train_flops) over the "
+                               "measured step time, against the dense MFMA peak of the GEMM dtype; the dominant "
+                               "kernel is k_tgemm (rocprof summary in profiles/)"}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(caps_np, lengths, B, args.cpu_budget)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 11
+#define AA_ABI_VERSION 12
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -301,14 +301,15 @@ AA_API int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, cons
  * about 2.3x faster, and the beams equal the exact ones except where two candidates are within the
  * logits' rounding difference of each other (measured: >= 98% of images at config 4).
  * Requires vocab <= 16384.  Replaces, for beam decoding, the greedy sampler's role in coco_eval
- * (code_src/tools/utils.py:171). */
+ * (code_src/tools/utils.py:171).  vocab_events (may be NULL): 2T hipEvent handles recorded on the
+ * stream around each step's vocab stage (logits + summaries), for per-launch timing. */
 #define AA_MAX_BEAM 8
 #define AA_BEAM_FAST 256 /* aa_beam_decode: bf16x3 logits with fused summaries instead of exact fp32 */
 AA_API size_t aa_beam_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T, int32_t K);
 AA_API int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int32_t K,
                           int32_t end_id, int64_t* ids, int64_t* seqs, float* scores, float* alpha,
                           float* beta, void* workspace, size_t workspace_bytes, int32_t flags,
-                          aa_stream_t stream);
+                          aa_stream_t stream, aa_event_t* vocab_events);
 
 /* Full fp32 vocab logits scores[B,V] = u W_m^T + b_m (AdaptiveBlock.mlp, adaptive_attention.py:132)
  * for given u = c_hat + h rows [B,H] (fp32 MFMA GEMM). */
