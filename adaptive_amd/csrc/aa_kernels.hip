@@ -543,18 +543,34 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
     const int img = 2 * blockIdx.x + (i >= C);
     if (img < B) a_g[(int64_t)img * C + (i - (i >= C ? C : 0))] = Ag[i];
   }
-  // epilogue: lane l holds column 16 nb + (l & 15), rows 16 rb + 4 (l >> 4) + i
+  // epilogue: lane l holds column 16 nb + (l & 15), rows 16 rb + 4 (l >> 4) + i.  Stored straight
+  // from the accumulators, every store instruction wrote 64-B row pieces (16 columns x 4 rows): 1.39x
+  // the V bytes left L2 (r01 PMC).  Instead each 16-row block goes through LDS ([16][H + 4] floats,
+  // aliasing the A stages) and leaves as whole rows: the workgroup's 98 rows are one contiguous
+  // 98 H-float run of V, written by 16-B lanes, 1 KB per wave instruction.
+  float* Vs = reinterpret_cast<float*>(&As[0][0][0]);
+  constexpr int VSP = H + 4;  // pitch: rows 4 apart land 16 banks apart (conflict-free transposed writes)
+  static_assert(16 * VSP * 4 <= sizeof(As), "V staging must fit in the A stages");
+  float bvs[NCB];
 #pragma unroll
-  for (int c = 0; c < NCB; ++c) {
-    const int col = (wave * NCB + c) * 16 + (lane & 15);
-    const float bv = bias[col];
+  for (int c = 0; c < NCB; ++c) bvs[c] = bias[(wave * NCB + c) * 16 + (lane & 15)];
 #pragma unroll
-    for (int rb = 0; rb < E4_RB; ++rb)
+  for (int rb = 0; rb < E4_RB; ++rb) {
+    __syncthreads();  // the previous block's rows were read out (rb = 0: the A stages are free)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = rb * 16 + 4 * (lane >> 4) + i, row = m0 + r;
-        if (r < E4_ROWS && row < M) V[(int64_t)row * H + col] = reluf_(acc[rb][c][i] + bv);
-      }
+    for (int c = 0; c < NCB; ++c) {
+      const int col = (wave * NCB + c) * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Vs[(4 * (lane >> 4) + i) * VSP + col] = reluf_(acc[rb][c][i] + bvs[c]);
+    }
+    __syncthreads();
+    constexpr int F4 = 16 * H / 4;  // float4s of the block
+#pragma unroll
+    for (int q = t; q < F4; q += 512) {
+      const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
+      if (tr < E4_ROWS && row < M)
+        *reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4) = *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4);
+    }
   }
 }
 
