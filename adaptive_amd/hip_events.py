@@ -26,6 +26,10 @@ def hip() -> ctypes.CDLL:
         lib.hipEventElapsedTime.restype = c_int
         lib.hipEventSynchronize.argtypes = [c_void_p]
         lib.hipEventSynchronize.restype = c_int
+        lib.hipStreamCreateWithFlags.argtypes = [POINTER(c_void_p), ctypes.c_uint]
+        lib.hipStreamCreateWithFlags.restype = c_int
+        lib.hipStreamDestroy.argtypes = [c_void_p]
+        lib.hipStreamDestroy.restype = c_int
         _hip = lib
     return _hip
 
@@ -73,3 +77,26 @@ class EventArray:
             self.close()
         except Exception:
             pass
+
+
+_raw_streams = {}
+
+
+def raw_streams(device, n: int):
+    """The first ``n`` of this process's fresh non-blocking HIP streams on ``device``
+    (hipStreamCreateWithFlags), as torch.cuda.ExternalStream objects.  HIP assigns each new stream a
+    hardware queue round-robin (GPU_MAX_HW_QUEUES, 4 by default), so streams created back to back land
+    on distinct queues -- unlike streams handed out by torch's pool, whose queues were fixed when the
+    pool was made.  They live as long as the process (torch's caching allocator may still record
+    events on them after their user is gone), and are reused by later callers."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    have = _raw_streams.setdefault(idx, [])
+    while len(have) < n:
+        h = c_void_p()
+        with torch.cuda.device(idx):
+            rc = hip().hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
+        if rc != 0:
+            raise RuntimeError(f"hipStreamCreateWithFlags failed: {rc}")
+        have.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx)))
+    return have[:n]

@@ -21,12 +21,21 @@ from .adaptive_attention import ATT, _Plan
 
 
 class _Slot:
-    def __init__(self, dev):
-        self.stream = torch.cuda.Stream(device=dev)
-        self.aux = torch.cuda.Stream(device=dev)  # the slot's side stream (aa_greedy_decode_aux)
+    def __init__(self, dev, stream):
+        self.stream = stream
+        self._aux = None
+        self.dev = dev
         self.ws = None
         self.plans = collections.OrderedDict()  # images key -> _Plan
         self.seen = set()
+
+    @property
+    def aux(self):
+        """The slot's side stream (aa_greedy_decode_aux's split LSTM steps), made on first use only:
+        an unused stream still takes a hardware queue in HIP's round-robin assignment."""
+        if self._aux is None:
+            self._aux = torch.cuda.Stream(device=self.dev)
+        return self._aux
 
 
 class DecodePipeline:
@@ -41,17 +50,23 @@ class DecodePipeline:
 
     MAX_PLANS = 2
 
-    def __init__(self, model, max_len: int = 20, depth: int = 2, graph: bool = False):
+    def __init__(self, model, max_len: int = 20, depth: int = 2, graph: bool = False, raw_streams: bool = True):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.model, self.T, self.depth, self.graph = model, int(max_len), int(depth), bool(graph)
+        self.raw_streams = bool(raw_streams)
         self._slots = None
         self._pending = collections.deque()
         self._n = 0
 
     def _slot(self, dev) -> _Slot:
         if self._slots is None:
-            self._slots = [_Slot(dev) for _ in range(self.depth)]
+            if self.raw_streams:  # fresh HIP streams: the slots land on distinct hardware queues
+                from .hip_events import raw_streams
+                streams = raw_streams(dev, self.depth)
+            else:
+                streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
+            self._slots = [_Slot(dev, st) for st in streams]
         return self._slots[self._n % self.depth]
 
     @torch.no_grad()
@@ -69,7 +84,8 @@ class DecodePipeline:
         ready.record()  # images (and any repack) are ready on the caller's stream
         s = slot.stream
         s.wait_event(ready)
-        slot.aux.wait_event(ready)
+        if m.split_lstm:
+            slot.aux.wait_event(ready)
         images.record_stream(s)
         flags = m._decode_flags()  # the same flags sampler() passes (fp32_encoder included)
         with torch.cuda.device(dev), torch.cuda.stream(s):

@@ -202,7 +202,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch kernels directly instead of replaying the "
                     "captured decode plan (hipGraph)")
     ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
-    ap.add_argument("--pipeline-depth", type=int, default=4, help="batches in flight in the headline region "
+    ap.add_argument("--pipeline-depth", type=int, default=3, help="batches in flight in the headline region "
                     "(adaptive_amd.pipeline.DecodePipeline: batch i+1 starts on its own stream while batch i "
                     "finishes); 1 = one sampler() call after another")
     ap.add_argument("--split-lstm", action="store_true", help="split LSTM steps: k_lstm_gemm on a side stream "
@@ -216,6 +216,8 @@ def main():
                     "buffer (MALL-resident; not the metric)")
     ap.add_argument("--replicate-buffer", action="store_true", help="diagnostics: distinct feature buffers holding "
                     "copies of the same batch (not the metric)")
+    ap.add_argument("--pool-streams", action="store_true", help="pipeline slots on torch pool streams instead of "
+                    "freshly created HIP streams")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -244,6 +246,7 @@ def main():
     # seeds 1.. for the same rows.
     nbuf = 1 if args.single_buffer else max(depth, 2)
     bufs = [synthetic_features(B, dev, seed=i, row0=rank * B) for i in range(nbuf)]
+    model.MAX_PLANS = max(model.MAX_PLANS, nbuf)  # one captured decode plan per resident buffer
     feats = bufs[0]
     if args.replicate_buffer:
         for b_ in bufs[1:]:
@@ -263,13 +266,13 @@ def main():
                                          graph=not args.no_graph)
         finish(i, ids)
 
-    pipe = DecodePipeline(model, max_len=T, depth=depth)
+    pipe = DecodePipeline(model, max_len=T, depth=depth, raw_streams=not args.pool_streams)
 
     def pipelined(n):
         for i, (ids, _, _) in enumerate(pipe.run(bufs[i % nbuf] for i in range(n))):
             finish(i, ids)
 
-    for i in range(max(args.warmup, 2 * nbuf)):  # every buffer seen twice: its decode plan is captured
+    for i in range(max(args.warmup, 3 * nbuf)):  # every buffer seen twice: its decode plan is captured
         step(i)
     pipelined(max(args.warmup, 2 * depth + 1))
     K = args.steps
@@ -370,9 +373,10 @@ def main():
     if dominant:
         kd = kernels[dominant]
         traffic = None
+        pmc_name = {"k_atten": "k_atten5", "k_vscreen": "k_vscreen2"}.get(dominant, dominant)  # rocprof names
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get(dominant, {}).get("hbm_bytes_per_launch")
+                traffic = json.load(f).get(pmc_name, {}).get("hbm_bytes_per_launch")
         except Exception:
             pass
         roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
