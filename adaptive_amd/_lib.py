@@ -17,12 +17,13 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 # AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
 LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libadaptive_amd.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
 DECODE_SCREEN64 = 8
 DECODE_ENC_V3 = 16
+DECODE_LISTS = 32
 BEAM_TILE128 = 64
 BEAM_FAST = 256
 TRAIN_BF16 = 128

@@ -223,6 +223,10 @@ class Encoder2Decoder(nn.Module):
         self.split_lstm = False
         # True: vocab screen on 64 x 64 tiles (k_vscreen) instead of 128 x 160 (k_vscreen2); same ids
         self.screen64 = False
+        # True: the vocab screen appends per-row candidate lists against a running max lower bound
+        # (k_vscreen3) and k_vrescore3 rescores them, instead of granule summaries (k_vscreen2) +
+        # k_vrescore; same ids, measured slower at B = 512, so off by default
+        self.vocab_lists = False
         # True: encoder V GEMM on k_enc_v3 (128 x 128 tiles) instead of k_enc_v4 (two images per
         # workgroup, all columns: the feature map is read once); same accuracy class
         self.enc_v3 = False
@@ -489,7 +493,7 @@ class Encoder2Decoder(nn.Module):
 
     def _lstm_flags(self) -> int:
         return ((0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
-                | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0))
+                | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0) | (_lib.DECODE_LISTS if self.vocab_lists else 0))
 
     def _lanes(self, n: int, dev) -> list:
         """n side streams on ``dev`` (created once, reused)."""

@@ -22,8 +22,14 @@ __device__ __forceinline__ void aa_ts(int kid, int slot) {
   }
 }
 #define AA_TS(kid, slot) aa_ts(kid, slot)
+// a value (e.g. a count) in slot 7 of the workgroup's record
+#define AA_TSV(kid, v)                                                                      \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && aa_ts_buf) aa_ts_buf[((size_t)(kid) * 2048 + blockIdx.x) * 16 + 7] = (v); \
+  } while (0)
 #else
 #define AA_TS(kid, slot)
+#define AA_TSV(kid, v)
 #endif
 
 constexpr int P = 49;          // attention width == 7x7 spatial locations (adaptive_attention.py:16-19)

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include "aa_common.hpp"
 
@@ -49,6 +50,9 @@ constexpr float CEPS = 0.0085f;
 constexpr float EPS_ABS = 1e-5f;
 constexpr int VS_TILE = 32;     // screen summary granule: one (lbmax, top-2 ub) per row per 32 columns
 constexpr int RS_CAP = 2048;    // candidate list capacity per row in k_vrescore (else full row)
+constexpr int LCAP = 64;        // k_vscreen3 -> k_vrescore3 list entries per row and step (else full row)
+constexpr int MK_LD = 1;        // row pitch of k_vscreen3's running lower bounds (uint32)
+constexpr int LCNT_LD = 1;      // row pitch of its list counts (uint32)
 // Exact fp32 logits (k_vocab and the rescoring) are NP_VOCAB independent fma chains over contiguous
 // K ranges (in the MFMA k order), combined as ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)), then + bias.
 constexpr int NP_VOCAB = 8;
@@ -1337,6 +1341,22 @@ __global__ void k_fill_tok(int64_t* __restrict__ tok, int B, int64_t v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B) tok[i] = v;
 }
+// Start of a greedy decode: <start> tokens, and the [T][B] argmax keys and running lower bounds
+// that k_vscreen3 accumulates by atomicMax cleared.
+// Start of a greedy decode: <start> tokens, and the [T][B] arrays that the vocab stage accumulates
+// into by atomics cleared -- argmax keys (k_vocab), running lower bounds and list counts
+// (k_vscreen3) -- by memory-side stores, like the atomics that follow (a plain store's line would
+// stay in this XCD's L2)
+__global__ void k_decode_init(int64_t* __restrict__ tok, int B, int64_t v, uint64_t* __restrict__ keys,
+                              uint32_t* __restrict__ mk, uint32_t* __restrict__ lcnt, int n) {
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  for (int i = i0; i < B; i += stride) tok[i] = v;
+  for (int i = i0; i < n; i += stride) {
+    __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mk + (int64_t)i * MK_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(lcnt + (int64_t)i * LCNT_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 __global__ void k_key_ids(const uint64_t* __restrict__ keys, int B, int64_t* __restrict__ ids, int ld) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B) ids[(int64_t)i * ld] = key_token(keys[i]);
@@ -1867,20 +1887,15 @@ __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0,
   }
 }
 
+// Main loop of the wide screen (k_vscreen2 / k_vscreen3): the tile's screened products
+// acc[b] = bf16(u) . bf16(w) of wave w's 32 rows x column block b (no bias), and un_s = ||u|| of the
+// tile's 128 rows.
 template <int H>
-__global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
-                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
-                                                  float4* __restrict__ summ) {
+__device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8* __restrict__ ua,
+                                             const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                             bf16x8 (*Ws)[SC2_STAGE], float* un_s, floatx16 (&acc)[SC2_NB]) {
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
-  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
-  __shared__ float un_s[SC2_BM];
-  AA_TS(2, 0);
-  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
-  const int L = xcd_remap(blockIdx.x, MT * NT);
-  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31;
-  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   // this wave's u fragments (row block m0 / 32 + wave) arrive one stage ahead, like the W stage:
   // a two-stage register ring instead of all KC chunks at once, so the kernel fits in 256 registers
   // (two waves per SIMD) and 40 KB of LDS -- two workgroups per CU, one per batch in flight
@@ -1906,14 +1921,11 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
 #pragma unroll
     for (int i = 0; i < PER; ++i) Ws[buf][t + 256 * i] = wr[i];
   };
-  // epilogue operands, loaded behind the fragments
+  // epilogue operand, loaded behind the fragments
   if (t < SC2_BM) {
     const int r = m0 + t;
     un_s[t] = unorm[r < B ? r : B - 1];
   }
-  const float bv0 = bias[n0 + li], bv1 = bias[n0 + 32 + li], bv2 = bias[n0 + 64 + li], bv3 = bias[n0 + 96 + li],
-              bv4 = bias[n0 + 128 + li];
-  floatx16 acc[SC2_NB];
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b)
 #pragma unroll
@@ -1937,8 +1949,27 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
       }
     }
   }
+}
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                  float4* __restrict__ summ) {
+  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
+  __shared__ float un_s[SC2_BM];
+  AA_TS(2, 0);
+  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NT);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31;
+  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  float bvs[SC2_NB];
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b) bvs[b] = bias[n0 + 32 * b + li];
+  floatx16 acc[SC2_NB];
+  screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc);
   AA_TS(2, 1);
-  const float bvs[SC2_NB] = {bv0, bv1, bv2, bv3, bv4};
   const int row0 = m0 + 32 * wave;
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b) {
@@ -1953,11 +1984,14 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
 // then the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) over xor-1/2/4 shuffles, then + bias.
 // Bit-identical to k_vocab (gemm_mainloop_np<.., NP_VOCAB>).  All 8 lanes return the logit.
 // u is read from LDS (urow), w straight from memory (each lane 4*32*per contiguous bytes).
+template <int HC = 0>  // HC > 0: H known at compile time (the K steps' loads issue together)
 __device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, const float* __restrict__ wrow, int H,
                                               float b, int lane8) {
-  const int per = H / (32 * NP_VOCAB);
+  const int per = (HC > 0 ? HC : H) / (32 * NP_VOCAB);
   const int k0 = lane8 * per * 32;
   float acc = 0.f;
+  constexpr int KU = HC > 0 ? HC / (32 * NP_VOCAB) : 1;
+#pragma unroll KU
   for (int ks = 0; ks < per; ++ks) {
     float4 w[8], u[8];
 #pragma unroll
@@ -2042,6 +2076,221 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
     if (ids) ids[(int64_t)b * T + t_step] = key_token(k);
   }
   AA_TS(3, 3);
+}
+
+// ---------------------------------------------------------------------------------------------
+// D3 (greedy path, AA_DECODE_LISTS): the wide screen writes per-row candidate LISTS instead of
+// per-granule summaries, and k_vrescore3 rescores each row's short list.  The summaries' path
+// (k_vscreen2 + k_vrescore, the default) reads 320 summaries per row to find M and then expands a
+// granule whose second-best bound reaches M to all 32 of its columns; here the screen decides per
+// column, against a running M (measured: the epilogue's atomic round trips -- publish/read M, claim
+// list slots -- cost more than the summaries' scan and expansion save):
+//   1. per row of the tile: lb = max over the tile's columns of A_n - E (the screen's bound, CEPS),
+//      published by an atomicMax into mk[row] (order-preserving u32 keys); the returned value gives
+//      M_cur = max of every lb published so far (<= M, the row's final max lb); while the workgroup
+//      has more than 32 candidates the running max is read once more (the row's other workgroups
+//      finish their main loops at about the same time and keep publishing);
+//   2. every column of the tile with A_n + E >= M_cur is appended to the row's list (atomicAdd on
+//      the row's count, entry = (order key of A_n + E) << 32 | column).
+// Since M_cur <= M, the lists hold every column k_vrescore would score (every column holding the
+// row's exact maximum passes A_n + E >= L_n >= M); k_vrescore3 keeps the entries whose bound reaches
+// the final M and scores them in exact fp32 (the fma order of k_vocab), so the ids equal
+// k_vscreen2 + k_vrescore's and AA_DECODE_EXACT_VOCAB's bit for bit, in any workgroup order.
+// mk and the counts are [T][B] arrays cleared once per decode; a list longer than LCAP makes its row
+// fall back to every column (correct, slow, never seen).
+// ---------------------------------------------------------------------------------------------
+
+// One transposing butterfly step of a float max over the 32 lanes of a column block (rows kept,
+// as screen_bfly).
+template <int M>
+__device__ __forceinline__ void max_bfly(float (&v)[16], int li) {
+  const bool hi = (li & M) != 0;
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    const float s = hi ? v[k] : v[k + M / 2], m = hi ? v[k + M / 2] : v[k];
+    v[k] = fmaxf(m, __uint_as_float(partner<M>(__float_as_uint(s))));
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_vscreen3(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                  uint32_t* __restrict__ mk, uint32_t* __restrict__ lcnt,
+                                                  uint64_t* __restrict__ lst, int nread) {
+  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
+  __shared__ float un_s[SC2_BM];
+  __shared__ float m_s[SC2_BM];
+  __shared__ int cnt_s[4];
+  AA_TS(2, 0);
+  const int NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NT);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31, lh = lane >> 5;
+  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  float bvs[SC2_NB];
+  float2 gsv[SC2_NB];
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b) {
+    bvs[b] = bias[n0 + 32 * b + li];
+    gsv[b] = gs[n0 / VS_TILE + b];
+  }
+  floatx16 acc[SC2_NB];
+  screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc);
+  AA_TS(2, 1);
+  // Bound per element: E = fma(||u||, alpha_g, beta_g) with alpha_g = W_g (CEPS + EPS_ABS) and
+  // beta_g = EPS_ABS B_g (the CEPS bound regrouped; the 1.0001 covers the regrouping's roundings, far
+  // inside CEPS's slack).  Columns past V get the bias -inf: their bounds are -inf (NaN on a garbage
+  // padding row), so they never count.  acc becomes the upper bound A + E.
+  float un16[16], lbm[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    un16[r] = un_s[32 * wave + acc_row(r, lane)];
+    lbm[r] = -INFINITY;
+  }
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b) {
+    const float al = gsv[b].x * ((CEPS + EPS_ABS) * 1.0001f), be = gsv[b].y * (EPS_ABS * 1.0001f);
+    const float bv = n0 + 32 * b + li < V ? bvs[b] : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float E = __builtin_fmaf(un16[r], al, be);
+      const float A = acc[b][r] + bv;
+      lbm[r] = fmaxf(lbm[r], A - E);
+      acc[b][r] = A + E;
+    }
+  }
+  max_bfly<16>(lbm, li);
+  max_bfly<8>(lbm, li);
+  max_bfly<4>(lbm, li);
+  max_bfly<2>(lbm, li);
+  // lane pairs (li, li ^ 1) now hold row rl of the wave's block: publish its lower bound and read the
+  // row's running max back (one atomic round trip)
+  const int rr = (li >> 1) & 15;
+  const int rl = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+  const int prow = m0 + 32 * wave + rl;
+  const bool pub = !(li & 1) && prow < B;
+  uint32_t cur = 0;
+  {
+    const float lb = fmaxf(lbm[0], __uint_as_float(partner<1>(__float_as_uint(lbm[0]))));
+    if (pub) {
+      const uint32_t mine = order_key(lb);
+      cur = atomicMax(mk + (int64_t)prow * MK_LD, mine);
+      cur = cur > mine ? cur : mine;
+    }
+  }
+  AA_TS(2, 2);
+  int reads = 1, tot = 0;
+  for (;;) {
+    if (!(li & 1)) m_s[32 * wave + rl] = prow < B ? key_value(cur) : __builtin_nanf("");  // NaN: no candidates
+    __syncthreads();
+    float M16[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) M16[r] = m_s[32 * wave + acc_row(r, lane)];
+    int n = 0;  // wave-uniform count
+#pragma unroll
+    for (int b = 0; b < SC2_NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) n += __popcll(__ballot(acc[b][r] >= M16[r]));  // false on NaN
+    if (lane == 0) cnt_s[wave] = n;
+    __syncthreads();
+    tot = (cnt_s[0] + cnt_s[1]) + (cnt_s[2] + cnt_s[3]);
+    if (tot <= 32 || reads >= nread) {  // uniform over the workgroup: append
+      // compact per wave into LDS entries (order key of the bound << 32 | local row << 8 | local
+      // column) in the dead W stages, then one atomicAdd per candidate, all in flight together,
+      // claims the list slots.  A wave with more than CW candidates (pathological ties) forces the
+      // overflowing rows to k_vrescore3's every-column fallback instead.
+      uint64_t* ent = reinterpret_cast<uint64_t*>(&Ws[0][0]);  // [4][CW]
+      constexpr int CW = (int)(sizeof(Ws) / sizeof(uint64_t) / 4);
+      const uint64_t below = (1ull << lane) - 1ull;
+      int k = 0;
+#pragma unroll
+      for (int b = 0; b < SC2_NB; ++b) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool c = acc[b][r] >= M16[r];
+          const uint64_t mask = __ballot(c);
+          if (__builtin_expect(mask != 0, 0)) {  // wave-uniform: the rare path
+            if (c) {
+              const int i = k + __popcll(mask & below);
+              if (i < CW)
+                ent[wave * CW + i] = ((uint64_t)order_key(acc[b][r]) << 32) | (uint32_t)((acc_row(r, lane) << 8) | (32 * b + li));
+              else
+                atomicAdd(lcnt + (int64_t)(m0 + 32 * wave + acc_row(r, lane)) * LCNT_LD, (uint32_t)LCAP + 1u);
+            }
+            k += __popcll(mask);
+          }
+        }
+      }
+      if (lane == 0) cnt_s[wave] = k < CW ? k : CW;
+      __syncthreads();
+      const int p1 = cnt_s[0], p2 = p1 + cnt_s[1], p3 = p2 + cnt_s[2], nl = p3 + cnt_s[3];
+      for (int i = t; i < nl; i += 256) {
+        const int w = (i >= p1) + (i >= p2) + (i >= p3);
+        const uint64_t e = ent[w * CW + i - (w == 0 ? 0 : w == 1 ? p1 : w == 2 ? p2 : p3)];
+        const int row = m0 + 32 * w + (int)((e >> 8) & 255u), col = n0 + (int)(e & 255u);
+        const uint32_t slot = atomicAdd(lcnt + (int64_t)row * LCNT_LD, 1u);
+        if (slot < (uint32_t)LCAP) lst[(int64_t)row * LCAP + slot] = (e & 0xFFFFFFFF00000000ull) | (uint32_t)col;
+      }
+      break;
+    }
+    ++reads;
+    if (pub) {
+      const uint32_t again = atomicMax(mk + (int64_t)prow * MK_LD, cur);  // = the current max (cur is published)
+      cur = again > cur ? again : cur;
+    }
+    __syncthreads();  // every wave has read m_s / cnt_s before they are rewritten
+  }
+  AA_TS(2, 3);
+  AA_TSV(2, tot + 1000 * reads);
+}
+
+// Rescoring of the lists (greedy path, default): one workgroup per row.  The entries whose bound
+// reaches the row's final M (mk) are the candidates -- every column that can hold the fp32 maximum
+// -- scored 32 per pass in exact fp32 (exact_logit8: k_vocab's fma order); first-index argmax ->
+// keys[row], ids[row, t].  A list that overflowed LCAP falls back to every column.
+template <int H>
+__global__ __launch_bounds__(256) void k_vrescore3(int B, int V, const float* __restrict__ u,
+                                                   const uint32_t* __restrict__ mk, const uint32_t* __restrict__ lcnt,
+                                                   const uint64_t* __restrict__ lst, const float* __restrict__ W,
+                                                   const float* __restrict__ bias, uint64_t* __restrict__ keys,
+                                                   int64_t* __restrict__ ids, int T, int t_step) {
+  __shared__ int cand[LCAP];
+  __shared__ int ncand;
+  __shared__ uint64_t wbest[4];
+  AA_TS(3, 0);
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t n = lcnt[(int64_t)row * LCNT_LD];
+  const uint32_t mkey = mk[(int64_t)row * MK_LD];
+  const bool all = n > (uint32_t)LCAP;
+  if (w == 0) {  // one wave compacts the list: keep the entries whose bound reaches M
+    const uint64_t e = lane < (int)n && !all ? lst[(int64_t)row * LCAP + lane] : 0ull;
+    const bool keep = lane < (int)n && !all && (uint32_t)(e >> 32) >= mkey;
+    const uint64_t mask = __ballot(keep);
+    if (keep) cand[__popcll(mask & ((1ull << lane) - 1ull))] = (int)(uint32_t)e;
+    if (lane == 0) ncand = __popcll(mask);
+  }
+  __syncthreads();
+  AA_TS(3, 1);
+  const int nc = all ? V : ncand;
+  const int g = t >> 3, lane8 = t & 7;
+  uint64_t best = 0;
+  for (int i = g; i < nc; i += 32) {
+    const int col = all ? i : cand[i];
+    const float x = exact_logit8<H>(u + (int64_t)row * H, W + (int64_t)col * H, H, bias[col], lane8);
+    const uint64_t k = argmax_key(x, col);
+    best = k > best ? k : best;
+  }
+  best = wave_max_u64(best);
+  if (lane == 0) wbest[w] = best;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t k = wbest[0];
+    for (int i = 1; i < 4; ++i) k = wbest[i] > k ? wbest[i] : k;
+    keys[row] = k;
+    if (ids) ids[(int64_t)row * T + t_step] = key_token(k);
+  }
+  AA_TS(3, 2);
 }
 
 // Exact fp32 logits of selected columns (cols [B][n], -1 = skip) -> out [B][n]; same arithmetic.
@@ -2487,6 +2736,8 @@ struct DecodeWS {
   bf16x8* hsp[2];
   float4* summ;
   uint64_t* keys;
+  uint32_t *mk, *lcnt;  // [T][B] running max lower bound and candidate count per row (k_vscreen3)
+  uint64_t* lst;        // [T][B][LCAP] candidate lists (k_vscreen3 -> k_vrescore3)
   int64_t* tok0;
 };
 static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* bytes) {
@@ -2510,6 +2761,9 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
+  w.mk = c.take<uint32_t>((size_t)T * B * MK_LD);
+  w.lcnt = c.take<uint32_t>((size_t)T * B * LCNT_LD);
+  w.lst = c.take<uint64_t>((size_t)T * B * LCAP);
   w.tok0 = c.take<int64_t>((size_t)B);
   *bytes = c.off;
   return w;
@@ -2542,7 +2796,7 @@ static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok,
       hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, \
                          xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);           \
     else                                                                                                     \
-      hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,     \
+      hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
                          p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);  \
   } while (0)
   switch (H) {
@@ -2573,7 +2827,7 @@ static void lstm_cell_launch(const Layout& L, const MP& p, int B, const int64_t*
 #define AA_CELL(H_)                                                                                           \
   do {                                                                                                        \
     if (par)                                                                                                  \
-      hipLaunchKernelGGL((k_lstm_cell<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,  \
+      hipLaunchKernelGGL((k_lstm_cell<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
                          p.table, xg, gates, c_in, par, p.wgs, h_out, hsp_out, c_out, s_buf, part);          \
     else                                                                                                      \
       hipLaunchKernelGGL((k_lstm_cell<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
@@ -2664,6 +2918,26 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   return launch_status();
 }
 
+// wide vocab-screen tiles (k_vscreen2 / k_vscreen3) when the padded vocabulary is whole 160-column
+// tiles (V = 10,123: 64 of them) and a wave's u fragments fit its registers
+static bool screen_wide(const Layout& L, int32_t flags) {
+  return L.Vp % SC2_BN == 0 && L.H <= 512 && !(flags & AA_DECODE_SCREEN64);
+}
+// the greedy decode's opt-in vocab stage: k_vscreen3 (screen + candidate lists) + k_vrescore3
+static bool greedy_lists(const Layout& L, int32_t flags) {
+  return (flags & AA_DECODE_LISTS) && !(flags & AA_DECODE_EXACT_VOCAB) && screen_wide(L, flags);
+}
+
+// reads of the running lower bound per row in k_vscreen3 (AA_SR_READS: tuning experiments)
+static int sr_reads() {
+  static int n = [] {
+    const char* e = getenv("AA_SR_READS");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
+  return n;
+}
+
 // The T-step loop over rows [r0, r0 + Bl) of the batch (every workspace array is row-indexed, so a
 // lane is the same loop on offset pointers; keys are [T][B]).
 // sg != nullptr: split LSTM steps -- k_lstm_gemm for step t+1 (it needs only h_t) runs on sg beside
@@ -2674,6 +2948,9 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
                        hipStream_t sg = nullptr) {
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   const int H = L.H, MT = (Bl + 63) / 64, NTn = L.Vp / VS_TILE;
+  const bool wide = screen_wide(L, flags);
+  // AA_DECODE_LISTS: the screen writes per-row candidate lists (k_vscreen3), rescored by k_vrescore3
+  const bool lists = greedy_lists(L, flags);
   const float* V = w.V + (size_t)r0 * P * H;
   const float* vwv = w.vwv + (size_t)r0 * P * PP;
   const float* xg = w.xg + (size_t)r0 * L.N5;
@@ -2713,6 +2990,8 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   }
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
+    // token of step t-1: ids[:, t-1] (written by the previous step) or, fused, the argmax keys of
+    // step t-1; <start> at t = 0
     // token of step t-1: ids[:, t-1] (written by the previous step), <start> at t = 0
     const int64_t* tok = t ? idsl + (t - 1) : w.tok0 + r0;
     const int tok_ld = t ? T : 1;
@@ -2755,22 +3034,41 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   hipLaunchKernelGGL(k_vscreen2<H_>, dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl, \
                      L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
                      reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
-      // wide tiles when the padded vocabulary is whole 160-column tiles (V = 10,123: 64 of them) and
-      // a wave's u fragments fit its registers
-      const bool wide = L.Vp % SC2_BN == 0 && H <= 512 && !(flags & AA_DECODE_SCREEN64);
-      switch (H) {
-        case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
-        case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
-        case 768: AA_SCREEN(768); break;
-        default: AA_SCREEN(1024); break;
+#define AA_SCREEN3(H_)                                                                                      \
+  hipLaunchKernelGGL(k_vscreen3<H_>, dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl, \
+                     L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
+                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, mkt, lct, lst, sr_reads())
+#define AA_RESCORE3(H_)                                                                                          \
+  hipLaunchKernelGGL(k_vrescore3<H_>, dim3(Bl), dim3(256), 0, s, Bl, L.V, u, mkt, lct, lst, p.mlp_w, p.mlp_b, kt, \
+                     idsl, T, t)
+      if (lists) {
+        uint32_t* mkt = w.mk + ((size_t)t * B + r0) * MK_LD;
+        uint32_t* lct = w.lcnt + ((size_t)t * B + r0) * LCNT_LD;
+        uint64_t* lst = w.lst + ((size_t)t * B + r0) * LCAP;
+        if (H == 256) AA_SCREEN3(256);
+        else AA_SCREEN3(512);
+        rec(sev, 2 * t + 1, s);
+        rec(rev, 2 * t, s);
+        if (H == 256) AA_RESCORE3(256);
+        else AA_RESCORE3(512);
+        rec(rev, 2 * t + 1, s);
+      } else {
+        switch (H) {
+          case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
+          case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
+          case 768: AA_SCREEN(768); break;
+          default: AA_SCREEN(1024); break;
+        }
+        rec(sev, 2 * t + 1, s);
+        rec(rev, 2 * t, s);
+        hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,
+                           idsl, T, t);
+        rec(rev, 2 * t + 1, s);
       }
 #undef AA_SCREEN
 #undef AA_SCREEN2
-      rec(sev, 2 * t + 1, s);
-      rec(rev, 2 * t, s);
-      hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,
-                         idsl, T, t);
-      rec(rev, 2 * t + 1, s);
+#undef AA_SCREEN3
+#undef AA_RESCORE3
     }
     if (split && !two && t + 1 < T) gemm(t + 1, s);
   }
@@ -2795,15 +3093,18 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
-  const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
-  if (exact) AA_TRY(hipMemsetAsync(w.keys, 0, (size_t)T * B * sizeof(uint64_t), s));
   if (!aux && n_lanes > 1) aux = (hipStream_t)lanes[1];
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, flags, s, aux);
   if (rc) return rc;
   hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
                      L.H, w.hsp[0]);
-  hipLaunchKernelGGL(k_fill_tok, dim3((B + 255) / 256), dim3(256), 0, s, w.tok0, B, (int64_t)1);  // <start>
+  {
+    const int n = T * B, nb = n > B ? n : B;
+    const int nblk = nb / 256 + 1;
+    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1, w.keys,
+                       w.mk, w.lcnt, n);
+  }
   // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
   int nl = n_lanes > 0 ? n_lanes : 1;
   const int tiles = (B + 63) / 64;

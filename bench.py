@@ -85,8 +85,11 @@ def kernel_costs(B: int, T: int) -> dict:
         "k_lstm_cell": ("hbm", lstm_cell_bytes(B)),
         "k_atten": ("hbm", atten_bytes_per_row() * B),
         "k_vscreen": ("mfma_bf16", f["k_vscreen"] * B),
+        "k_vscreen3": ("mfma_bf16", f["k_vscreen"] * B),  # + the candidate lists (not priced)
         # per row: 320 granule summaries + u + the winning W_m row + id/key out (candidate count varies)
         "k_vrescore": ("hbm", B * ((V + 127) // 128 * 4 * 16 + 4 * H + 4 * H + 16)),
+        # per row: u + the winning W_m row + id/key out (the list and the other candidates vary)
+        "k_vrescore3": ("hbm", B * (4 * H + 4 * H + 16)),
     }
 
 
@@ -169,7 +172,7 @@ def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
             "cpus": cpus}
 
 
-def path_ideal_seconds(B: int, T: int, Vp: int = 10240) -> dict:
+def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True) -> dict:
     """Executed work of one decode priced at each kernel's own ceiling: bf16x3 GEMMs
     at bf16 peak / 6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen (all Vp padded
     columns) at the bf16 peak, the attention and rescoring at HBM peak for their bytes.  The sum is
@@ -183,8 +186,9 @@ def path_ideal_seconds(B: int, T: int, Vp: int = 10240) -> dict:
         "k_lstm": T * (f["k_lstm_gemm"] * B / PEAK_X3 + f["proj"] * B / PEAK_FP32),
         "k_atten": T * atten_bytes_per_row() * B / PEAK_HBM,
         "k_vscreen": T * 2 * H * Vp * B / PEAK_BF16,
-        "k_vrescore": T * kernel_costs(B, T)["k_vrescore"][1] / PEAK_HBM,
     }
+    rescore = "k_vrescore3" if lists else "k_vrescore"
+    parts[rescore] = T * kernel_costs(B, T)[rescore][1] / PEAK_HBM
     return {"total": sum(parts.values()), "parts": parts}
 
 
@@ -209,6 +213,8 @@ def main():
                     "+ k_lstm_cell instead of the one-launch k_lstm (same results; slower at B=512)")
     ap.add_argument("--screen64", action="store_true", help="vocab screen on 64x64 tiles (k_vscreen) instead of "
                     "128x160 (k_vscreen2)")
+    ap.add_argument("--vocab-lists", action="store_true", help="vocab stage as per-row candidate lists (k_vscreen3) "
+                    "+ k_vrescore3 instead of granule summaries (k_vscreen2) + k_vrescore (same ids)")
     ap.add_argument("--enc-v3", action="store_true", help="encoder V GEMM on k_enc_v3 (128x128 tiles) instead of "
                     "k_enc_v4 (two images per workgroup, all columns)")
     ap.add_argument("--no-d2h", action="store_true", help="diagnostics: leave the ids on the device (not the metric)")
@@ -237,6 +243,9 @@ def main():
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
     model.split_lstm = args.split_lstm
     model.screen64 = args.screen64
+    model.vocab_lists = args.vocab_lists
+    lists = args.vocab_lists and not args.screen64
+    screen_name, rescore_name = ("k_vscreen3", "k_vrescore3") if lists else ("k_vscreen", "k_vrescore")
     model.enc_v3 = args.enc_v3
     enc_name = "k_enc_v3" if args.enc_v3 else "k_enc_v4"
     depth = max(1, args.pipeline_depth)
@@ -329,7 +338,7 @@ def main():
         lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
         enc_names = ("k_avgpool", enc_name, "k_enc_heads" if args.enc_v3 else "k_enc_heads3", "k_gemm_bias(VWv)",
                      "k_gemm_bias(x_g)")
-        per = {k: [] for k in enc_names + (lstm, "k_atten", "k_vscreen", "k_vrescore")}
+        per = {k: [] for k in enc_names + (lstm, "k_atten", screen_name, rescore_name)}
         if not args.enc_v3:
             del per["k_avgpool"]  # fused into k_enc_v4 (its trace pair is empty)
         if model.split_lstm:
@@ -343,8 +352,8 @@ def main():
             if model.split_lstm:
                 per["k_lstm_gemm"] += ev["gemm"].pair_durations_ms()
             per["k_atten"] += ev["atten"].pair_durations_ms()
-            per["k_vscreen"] += ev["screen"].pair_durations_ms()
-            per["k_vrescore"] += ev["rescore"].pair_durations_ms()
+            per[screen_name] += ev["screen"].pair_durations_ms()
+            per[rescore_name] += ev["rescore"].pair_durations_ms()
         costs = kernel_costs(B, T)
         for k, ds in per.items():
             avg_ms = float(np.mean(ds))
@@ -365,7 +374,8 @@ def main():
                                      "(fp32-accurate); algorithmic fp32 FLOPs priced against bf16 peak / 6")
                 if bound == "mfma_bf16":
                     entry["note"] = ("2HV vocab contraction on bf16 MFMA under a rigorous error bound (exact fp32 "
-                                     "rescoring of the candidates in k_vrescore); priced against the dense bf16 peak")
+                                     "rescoring of the candidates in " + rescore_name + "); priced against the "
+                                     "dense bf16 peak")
             entry["frac"] = entry["achieved"] / entry["peak"]
             kernels[k] = entry
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
@@ -383,7 +393,7 @@ def main():
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"]}
 
-    ideal = path_ideal_seconds(B, T)
+    ideal = path_ideal_seconds(B, T, lists=lists)
     out = {
         "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -398,6 +408,8 @@ def main():
                    # how each region launches: the pipeline's slots launch kernels directly (its
                    # graph=False default); the sequential region replays captured decode plans
                    "hip_graph": {"pipelined": pipe.graph, "sequential": not args.no_graph},
+                   "vocab_stage": "k_vscreen3 (screen + per-row candidate lists) + k_vrescore3" if lists
+                   else "k_vscreen2/k_vscreen (granule summaries) + k_vrescore",
                    "lstm_step": "split (k_lstm_gemm on a side stream + k_lstm_cell)" if model.split_lstm
                    else "fused (k_lstm)",
                    "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy"},

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 12
+#define AA_ABI_VERSION 13
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -120,8 +120,10 @@ typedef struct aa_model {
  * aa_greedy_decode records event [2i] before and [2i+1] after the i-th launch of that kernel:
  *   encoder_events: 2*AA_TRACE_ENCODER_KERNELS events, launches in the order
  *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
- *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen
- *                   (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused then);
+ *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen2 /
+ *                   k_vscreen (k_vscreen3 under AA_DECODE_LISTS, k_vocab under
+ *                   AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (k_vrescore3; unused under
+ *                   AA_DECODE_EXACT_VOCAB);
  *                   lstm = k_lstm, or k_lstm_cell when the step is split (aa_greedy_decode_aux);
  *   gemm_events:    2*T events, launch i = k_lstm_gemm of step i (split steps only; recorded on
  *                   the aux stream). */
@@ -185,6 +187,9 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
                                     the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v4) */
 #define AA_BEAM_TILE128 64 /* beam search: vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256
                              (k_vbeam5); identical logits */
+#define AA_DECODE_LISTS 32 /* greedy: the vocab screen appends per-row candidate lists against a running max
+                             lower bound (k_vscreen3) and k_vrescore3 rescores them, instead of granule
+                             summaries (k_vscreen2) + k_vrescore; same ids (measured slower at B = 512) */
 #define AA_DECODE_ENC_V3 16 /* V on the 128 x 128-tile bf16x3 kernel (k_enc_v3) instead of k_enc_v4 (one
                                workgroup per two images, all H columns; H in {256, 512}) */
 

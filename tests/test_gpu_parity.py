@@ -325,3 +325,36 @@ def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device)
     b = m.sampler(feats, max_len=T, exact_vocab=True)
     assert torch.equal(a[0], b[0])
     assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("B,lanes", [(512, 1), (300, 1), (77, 1), (4, 1), (512, 2)])
+def test_vocab_lists_equal_summaries(model, gpu_device, B, lanes):
+    """k_vscreen3 + k_vrescore3 (per-row candidate lists decided against the running max lower bound)
+    == k_vscreen2 + k_vrescore (granule summaries): ids, alpha, beta identical."""
+    feats = torch.from_numpy(synth.make_features(B, seed=43)).to(gpu_device)
+    ref = model.sampler(feats, max_len=13, graph=False, lanes=lanes)
+    model.vocab_lists = True
+    try:
+        got = model.sampler(feats, max_len=13, graph=False, lanes=lanes)
+    finally:
+        model.vocab_lists = False
+    torch.cuda.synchronize()
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+
+
+@pytest.mark.parametrize("lists", [False, True])
+def test_all_columns_tied_rescore_overflow(gpu_device, lists):
+    """W_m = 0, b_m = 0: every logit is exactly 0, so every column is a candidate (k_vscreen3's
+    per-row lists and k_vrescore's candidate list overflow into their all-columns fallbacks).  The
+    first index (0) must win everywhere, as torch's max(2)[1]."""
+    m = _model()
+    with torch.no_grad():
+        m.decoder.adaptive.mlp.weight.zero_()
+        m.decoder.adaptive.mlp.bias.zero_()
+    m.vocab_lists = lists
+    feats = torch.from_numpy(synth.make_features(130, seed=4)).to(gpu_device)
+    ids, _, _ = m.sampler(feats, max_len=3, graph=False)
+    assert torch.equal(ids, torch.zeros_like(ids))
+    ex, _, _ = m.sampler(feats, max_len=3, graph=False, exact_vocab=True)
+    assert torch.equal(ex, ids)

@@ -19,8 +19,10 @@ from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
 
 KERNELS = {0: ("k_lstm", ["entry", "gemm done", "tile summed", "cell stored", "exit"]),
            1: ("k_atten5", ["entry", "proj barrier", "scores barrier", "softmax barrier", "exit"]),
-           2: ("k_vscreen2", ["entry", "mainloop done", "exit"]),
-           3: ("k_vrescore", ["entry", "M reduced", "candidates", "exit"])}
+           2: (("k_vscreen2", ["entry", "mainloop done", "exit"]) if not os.environ.get("AA_VOCAB_LISTS") else
+               ("k_vscreen3", ["entry", "mainloop done", "M read", "appended"])),
+           3: (("k_vrescore", ["entry", "M reduced", "candidates", "exit"]) if not os.environ.get("AA_VOCAB_LISTS") else
+               ("k_vrescore3", ["entry", "listed", "exit"]))}
 
 
 def main():
@@ -29,6 +31,7 @@ def main():
     lib.aa_ts_setup.argtypes = [ctypes.c_void_p]
     buf = torch.zeros(5 * 2048 * 16, dtype=torch.int64, device=dev)
     m = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
+    m.vocab_lists = bool(os.environ.get("AA_VOCAB_LISTS"))
     feats = synthetic_features(512, dev, seed=0)
     for rep in range(3):
         buf.zero_()
@@ -40,6 +43,8 @@ def main():
     for kid, (name, marks) in KERNELS.items():
         t = ts[kid, :, :len(marks)].astype(np.int64)
         ok = t[:, 0] > 0
+        if not ok.any():
+            continue
         t = t[ok]
         tc = ts[kid, :, 8:8 + len(marks)].astype(np.int64)[ok]
         span_rt = (t[:, -1] - t[:, 0]).astype(np.float64)
@@ -47,6 +52,11 @@ def main():
         t0 = t[:, 0].min()
         rel = (t - t0) * 0.01  # 100 MHz ticks -> us
         print(f"{name}: {ok.sum()} workgroups; span {rel.max():.2f} us; shader clock {clk:.2f} GHz")
+        if name == "k_vscreen3":
+            v = ts[kid, :, 7][ok]
+            cnt, rd = v % 1000, v // 1000
+            print(f"   candidates per workgroup: mean {cnt.mean():.1f}  p90 {np.quantile(cnt, 0.9):.0f}  max {cnt.max()};"
+                  f"  running-max reads: mean {rd.mean():.2f} max {rd.max()}")
         for i, mk in enumerate(marks):
             q = np.quantile(rel[:, i], [0.0, 0.5, 0.9, 1.0])
             d = np.quantile(rel[:, i] - rel[:, i - 1], [0.5, 0.9]) if i else (0, 0)
