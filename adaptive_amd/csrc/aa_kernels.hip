@@ -2016,12 +2016,15 @@ __device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, co
 // = idx1 of granules with ub1 >= M, plus every column of granules with ub2 >= M (two candidates in
 // one granule).  32 candidates are scored per pass (8 lanes each, exact_logit8); first-index argmax
 // -> keys[row], ids[row, t].  A list longer than RS_CAP falls back to every column (correct, slow).
+// (Tried: re-screening a ub2 >= M granule's 32 columns in bf16 here, sequentially or 64 columns per
+// round, and scoring only those within the bound: fewer exact logits, but slower overall.)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, const float* __restrict__ u,
+template <int H>
+__global__ __launch_bounds__(256) void k_vrescore(int B, int V, int Vp, const float* __restrict__ u,
                                                   const float4* __restrict__ summ, const float* __restrict__ W,
                                                   const float* __restrict__ bias, uint64_t* __restrict__ keys,
                                                   int64_t* __restrict__ ids, int T, int t_step) {
-  __shared__ __attribute__((aligned(16))) float urow[MAX_H];
+  __shared__ __attribute__((aligned(16))) float urow[H];
   __shared__ int cand[RS_CAP];
   __shared__ int ncand;
   __shared__ float wmax[4];
@@ -2032,15 +2035,19 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
   for (int d = 4 * t; d < H; d += 1024) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
   if (t == 0) ncand = 0;
   const float4* sm = summ + (int64_t)b * NTn;
-  float mlb = -INFINITY;
-  for (int i = t; i < NTn; i += 256) mlb = fmaxf(mlb, sm[i].x);
+  // a thread's first two summaries stay in registers between the max and the selection (any
+  // further ones, NTn > 512, are read again)
+  float4 s0 = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f), s1 = s0;
+  if (t < NTn) s0 = sm[t];
+  if (t + 256 < NTn) s1 = sm[t + 256];
+  float mlb = fmaxf(s0.x, s1.x);
+  for (int i = t + 512; i < NTn; i += 256) mlb = fmaxf(mlb, sm[i].x);
   mlb = wave_max(mlb);
   if (lane == 0) wmax[w] = mlb;
   __syncthreads();
   AA_TS(3, 1);
   mlb = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
-  for (int i = t; i < NTn; i += 256) {
-    const float4 s = sm[i];
+  auto select = [&](const float4& s, int i) {
     if (s.z >= mlb) {  // >= 2 candidates in this granule: take all of its columns
       const int pos = atomicAdd(&ncand, VS_TILE);
       for (int c = 0; c < VS_TILE; ++c)
@@ -2049,7 +2056,10 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
       const int pos = atomicAdd(&ncand, 1);
       if (pos < RS_CAP) cand[pos] = __float_as_int(s.w);
     }
-  }
+  };
+  if (t < NTn) select(s0, t);
+  if (t + 256 < NTn) select(s1, t + 256);
+  for (int i = t + 512; i < NTn; i += 256) select(sm[i], i);
   __syncthreads();
   AA_TS(3, 2);
   const bool all = ncand > RS_CAP;
@@ -2060,6 +2070,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int H, int V, int Vp, c
     int col = all ? i : cand[i];
     const bool ok = col < V;
     col = ok ? col : V - 1;
+    // (the K steps' loads one after the other: measured faster here than all issued together)
     const float x = exact_logit8(urow, W + (int64_t)col * H, H, bias[col], lane8);
     if (ok) {
       const uint64_t k = argmax_key(x, col);
@@ -3061,8 +3072,15 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
         }
         rec(sev, 2 * t + 1, s);
         rec(rev, 2 * t, s);
-        hipLaunchKernelGGL(k_vrescore, dim3(Bl), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt,
-                           idsl, T, t);
+#define AA_RESCORE(H_)                                                                                          \
+  hipLaunchKernelGGL(k_vrescore<H_>, dim3(Bl), dim3(256), 0, s, Bl, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt, idsl, T, t)
+        switch (H) {
+          case 256: AA_RESCORE(256); break;
+          case 512: AA_RESCORE(512); break;
+          case 768: AA_RESCORE(768); break;
+          default: AA_RESCORE(1024); break;
+        }
+#undef AA_RESCORE
         rec(rev, 2 * t + 1, s);
       }
 #undef AA_SCREEN
