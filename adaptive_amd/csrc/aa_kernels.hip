@@ -765,6 +765,20 @@ __device__ __forceinline__ void x3_step(floatx16& acc, const bf16x8 (&a)[3], con
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], acc, 0, 0, 0);
 }
 
+// Two-accumulator form (the lean k_lstm / k_lstm_gemm GEMMs): the three small products (i + j = 2)
+// go to one chain and the three large ones (i + j <= 1) to another, summed once at the end -- two
+// independent MFMA chains per wave instead of one dependent chain of 6 per chunk (sequential decode
+// +3 % in A/B; at least as accurate: the small terms no longer meet the large running sum chunk by
+// chunk).
+__device__ __forceinline__ void x3_step2(floatx16& sm, floatx16& bg, const bf16x8 (&a)[3], const bf16x8 (&w)[3]) {
+  sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], sm, 0, 0, 0);
+  bg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], bg, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], sm, 0, 0, 0);
+  bg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], bg, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], sm, 0, 0, 0);
+  bg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], bg, 0, 0, 0);
+}
+
 constexpr int LS_CP = 68;  // k_lstm LDS tile pitch (floats): conflict-free cell reads
 
 // Cell epilogue shared by k_lstm (GEMM + cell in one launch) and k_lstm_cell (cell of a GEMM done
@@ -964,9 +978,9 @@ __device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* 
   const bf16x8* af = a ? af1 : af0;
   const bf16x8* wf = c ? wf1 : wf0;
   const int kc0 = kh * per;
-  floatx16 acc;
+  floatx16 acc, acc2;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
   bf16x8 fa[NR][3], fw[NR][3];
   auto load = [&](int slot, int kc) {
 #pragma unroll
@@ -988,13 +1002,15 @@ __device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* 
 #ifdef AA_EXP_NOMFMA  // tools/ktrace experiment: loads only (wrong results)
     acc[0] += (float)fa[i % NR][0][0] + (float)fw[i % NR][0][0];
 #else
-    x3_step(acc, fa[i % NR], fw[i % NR]);
+    x3_step2(acc2, acc, fa[i % NR], fw[i % NR]);
 #endif
 #ifndef AA_EXP_NOLOAD  // tools/ktrace experiment: MFMAs on the first NR chunks only (wrong results)
     if (i + NR < per) load(i % NR, kc0 + i + NR);
 #endif
     __builtin_amdgcn_sched_barrier(0);
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += acc2[r];  // large-product chain + small-product chain
   const int li = lane & 31, lh = lane >> 5;
   float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;
   if (kh) {
@@ -1075,9 +1091,9 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
       fw[set][q] = sb[(6 + 3 * c + q) * 64];
     }
   };
-  floatx16 acc;
+  floatx16 acc, acc2;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1107,10 +1123,12 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
 #ifdef AA_EXP_NOMFMA
     acc[0] += (float)fa[set][0][0] + (float)fw[set][0][0];
 #else
-    x3_step(acc, fa[set], fw[set]);
+    x3_step2(acc2, acc, fa[set], fw[set]);
 #endif
     __builtin_amdgcn_sched_barrier(0);
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += acc2[r];  // large-product chain + small-product chain
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ring free: Pt aliases it
   const int li = lane & 31, lh = lane >> 5;
   float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;

@@ -2,7 +2,7 @@
 
 Run in the survey/build container only (``/root/reference`` does not exist on the GPU box):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]
 
 How the reference is driven:
 * ``torchvision`` is absent: a stub module whose ``resnet152`` returns an empty ``nn.Module``, so
@@ -88,7 +88,7 @@ def run(m, feats, T, scores_hook=False):
     return ids.numpy(), alpha.numpy(), beta.numpy(), scores.numpy(), margin
 
 
-def main():
+def main(only=None):
     torch.set_num_threads(8)
     aa = load_reference()
     manifest = {"reference": "wzn0828/Adaptive code_src/models/adaptive_attention.py Encoder2Decoder.sampler",
@@ -101,7 +101,12 @@ def main():
         ("ref_b512", 123, 0.0, 0, 512, "ids"),
         ("biased_b16", 99, 0.02, 5, 16, "full"),
     ]
+    if only:  # regenerate some cases only; the manifest keeps the others' entries
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest["cases"] = json.load(f)["cases"]
     for name, wseed, noise, fseed, B, keep in cases:
+        if only and name not in only:
+            continue
         state = synth.make_weights(wseed, bias_noise=noise)
         feats = synth.make_features(B, seed=fseed)
         m = build(aa, state)
@@ -109,6 +114,8 @@ def main():
         out = {"ids": ids.astype(np.int16), "beta": beta.astype(np.float32), "margin": margin.astype(np.float32)}
         if keep in ("full", "alpha"):
             out["alpha"] = alpha.astype(np.float32)
+        if keep == "ids":  # alpha of every 4th row (each 64-row tile of the decode kernels sampled)
+            out["alpha_s4"] = alpha[::4].astype(np.float32)
         if keep == "full":
             # full logits of rows 0,1 at steps 0,1 and step-0 logits of every row
             out["scores_r01_t01"] = scores[:2, :2].astype(np.float32)
@@ -130,4 +137,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])  # optional case names

@@ -163,6 +163,8 @@ def test_greedy_b512_vs_reference_golden(gpu_device):
     mism = np.argwhere(ids != g["ids"])
     assert mism.size == 0, f"{len(mism)} token mismatches, first at {mism[:3].tolist()}, margin there {g['margin'][tuple(mism[0])]}"
     np.testing.assert_allclose(beta.cpu().numpy(), g["beta"], atol=ATT_TOL, rtol=0)
+    # alpha of every 4th row (all eight 64-row tiles of the step kernels), pinned by the reference
+    np.testing.assert_allclose(alpha.cpu().numpy()[::4], g["alpha_s4"], atol=ATT_TOL, rtol=0)
 
 
 def test_batch_invariance(model, gpu_device):

@@ -35,9 +35,10 @@ def test_oracle_matches_reference_golden(case, manifest):
 def test_oracle_b512_ids_match_reference_golden():
     g = load_golden("ref_b512")
     feats = synth.make_features(512)
-    ids, _, beta = OracleModel(synth.make_weights(123)).sampler(torch.from_numpy(feats), max_len=20)
+    ids, alpha, beta = OracleModel(synth.make_weights(123)).sampler(torch.from_numpy(feats), max_len=20)
     assert np.array_equal(ids.numpy(), g["ids"].astype(np.int64))
     np.testing.assert_allclose(beta.numpy(), g["beta"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(alpha.numpy()[::4], g["alpha_s4"], atol=1e-6, rtol=0)  # every 4th row
 
 
 def test_oracle_row_independence():
