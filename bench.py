@@ -234,10 +234,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit(f"--gpus {args.gpus} needs a torchrun launch with {args.gpus} processes")
+    # AA_DIST_BACKEND=gloo: rehearsal of the N > 1 path with several ranks sharing the visible GPUs
+    # (ids gathered through the host; not a scaling measurement)
+    backend = os.environ.get("AA_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     B, T = args.batch, args.max_len
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
@@ -402,7 +410,8 @@ def main():
                 "weights of the reference architecture (adaptive_amd/synth.py, seed 123)",
         "config": {"workload": f"greedy decode (Encoder2Decoder.sampler) B={B}/GPU, max_len={T}",
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
-                   "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else ""),
+                   "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else "")
+                   + ("" if backend == "nccl" else f" ({backend} rehearsal)"),
                    "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
                    "batches_in_flight": depth, "feature_buffers": nbuf,
                    # how each region launches: the pipeline's slots launch kernels directly (its
