@@ -1369,10 +1369,10 @@ __global__ void k_decode_init(int64_t* __restrict__ tok, int B, int64_t v, uint6
                               uint32_t* __restrict__ mk, uint32_t* __restrict__ lcnt, int n) {
   const int i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   for (int i = i0; i < B; i += stride) tok[i] = v;
-  for (int i = i0; i < n; i += stride) {
-    __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(mk + (int64_t)i * MK_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(lcnt + (int64_t)i * LCNT_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = i0; i < n; i += stride) {  // (each array only when the decode's vocab stage uses it)
+    if (keys) __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mk) __hip_atomic_store(mk + (int64_t)i * MK_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lcnt) __hip_atomic_store(lcnt + (int64_t)i * LCNT_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 __global__ void k_key_ids(const uint64_t* __restrict__ keys, int B, int64_t* __restrict__ ids, int ld) {
@@ -3136,10 +3136,13 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
                      L.H, w.hsp[0]);
   {
-    const int n = T * B, nb = n > B ? n : B;
+    // atomics accumulate into keys (k_vocab) and, for the lists, mk / lcnt; the default vocab stage
+    // writes every key it produces, so it needs no clearing
+    const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0, lists = greedy_lists(L, flags);
+    const int n = exact || lists ? T * B : 0, nb = n > B ? n : B;
     const int nblk = nb / 256 + 1;
-    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1, w.keys,
-                       w.mk, w.lcnt, n);
+    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1,
+                       exact ? w.keys : nullptr, lists ? w.mk : nullptr, lists ? w.lcnt : nullptr, n);
   }
   // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
   int nl = n_lanes > 0 ? n_lanes : 1;
