@@ -2037,34 +2037,40 @@ __device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, co
 // (Tried: re-screening a ub2 >= M granule's 32 columns in bf16 here, sequentially or 64 columns per
 // round, and scoring only those within the bound: fewer exact logits, but slower overall.)
 // ---------------------------------------------------------------------------------------------
+#ifndef AA_RS_THREADS
+#define AA_RS_THREADS 256
+#endif
+constexpr int RS_NT = AA_RS_THREADS, RS_NW = RS_NT / 64;
 template <int H>
-__global__ __launch_bounds__(256) void k_vrescore(int B, int V, int Vp, const float* __restrict__ u,
+__global__ __launch_bounds__(RS_NT) void k_vrescore(int B, int V, int Vp, const float* __restrict__ u,
                                                   const float4* __restrict__ summ, const float* __restrict__ W,
                                                   const float* __restrict__ bias, uint64_t* __restrict__ keys,
                                                   int64_t* __restrict__ ids, int T, int t_step) {
   __shared__ __attribute__((aligned(16))) float urow[H];
   __shared__ int cand[RS_CAP];
   __shared__ int ncand;
-  __shared__ float wmax[4];
-  __shared__ uint64_t wbest[4];
+  __shared__ float wmax[RS_NW];
+  __shared__ uint64_t wbest[RS_NW];
   AA_TS(3, 0);
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int NTn = Vp / VS_TILE;
-  for (int d = 4 * t; d < H; d += 1024) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
+  for (int d = 4 * t; d < H; d += 4 * RS_NT) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
   if (t == 0) ncand = 0;
   const float4* sm = summ + (int64_t)b * NTn;
   // a thread's first two summaries stay in registers between the max and the selection (any
-  // further ones, NTn > 512, are read again)
+  // further ones are read again)
   float4 s0 = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f), s1 = s0;
   if (t < NTn) s0 = sm[t];
-  if (t + 256 < NTn) s1 = sm[t + 256];
+  if (t + RS_NT < NTn) s1 = sm[t + RS_NT];
   float mlb = fmaxf(s0.x, s1.x);
-  for (int i = t + 512; i < NTn; i += 256) mlb = fmaxf(mlb, sm[i].x);
+  for (int i = t + 2 * RS_NT; i < NTn; i += RS_NT) mlb = fmaxf(mlb, sm[i].x);
   mlb = wave_max(mlb);
   if (lane == 0) wmax[w] = mlb;
   __syncthreads();
   AA_TS(3, 1);
-  mlb = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  mlb = wmax[0];
+#pragma unroll
+  for (int i = 1; i < RS_NW; ++i) mlb = fmaxf(mlb, wmax[i]);
   auto select = [&](const float4& s, int i) {
     if (s.z >= mlb) {  // >= 2 candidates in this granule: take all of its columns
       const int pos = atomicAdd(&ncand, VS_TILE);
@@ -2076,15 +2082,15 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int V, int Vp, const fl
     }
   };
   if (t < NTn) select(s0, t);
-  if (t + 256 < NTn) select(s1, t + 256);
-  for (int i = t + 512; i < NTn; i += 256) select(sm[i], i);
+  if (t + RS_NT < NTn) select(s1, t + RS_NT);
+  for (int i = t + 2 * RS_NT; i < NTn; i += RS_NT) select(sm[i], i);
   __syncthreads();
   AA_TS(3, 2);
   const bool all = ncand > RS_CAP;
   const int n = all ? V : ncand;
   const int g = t >> 3, lane8 = t & 7;
   uint64_t best = 0;
-  for (int i = g; i < n; i += 32) {
+  for (int i = g; i < n; i += RS_NT / 8) {
     int col = all ? i : cand[i];
     const bool ok = col < V;
     col = ok ? col : V - 1;
@@ -2100,7 +2106,7 @@ __global__ __launch_bounds__(256) void k_vrescore(int B, int V, int Vp, const fl
   __syncthreads();
   if (t == 0) {
     uint64_t k = wbest[0];
-    for (int i = 1; i < 4; ++i) k = wbest[i] > k ? wbest[i] : k;
+    for (int i = 1; i < RS_NW; ++i) k = wbest[i] > k ? wbest[i] : k;
     keys[b] = k;
     if (ids) ids[(int64_t)b * T + t_step] = key_token(k);
   }
@@ -3091,7 +3097,7 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
         rec(sev, 2 * t + 1, s);
         rec(rev, 2 * t, s);
 #define AA_RESCORE(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vrescore<H_>, dim3(Bl), dim3(256), 0, s, Bl, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt, idsl, T, t)
+  hipLaunchKernelGGL(k_vrescore<H_>, dim3(Bl), dim3(RS_NT), 0, s, Bl, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt, idsl, T, t)
         switch (H) {
           case 256: AA_RESCORE(256); break;
           case 512: AA_RESCORE(512); break;

@@ -845,7 +845,7 @@ extern "C" int kb_time(const aa_model* m, const float* feats, void* ws, int B, i
                          L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,
                          reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ);
     } else if (!strcmp(which, "vrescore")) {
-      hipLaunchKernelGGL(k_vrescore, dim3(B), dim3(256), 0, s, B, L.H, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
+      hipLaunchKernelGGL(k_vrescore<512>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt,
                          (int64_t*)nullptr, T, t);
     } else if (!strcmp(which, "enc_v3")) {
       const int M = B * P;
