@@ -24,6 +24,7 @@ DECODE_FUSED_LSTM = 4
 DECODE_SCREEN64 = 8
 DECODE_ENC_V3 = 16
 DECODE_LISTS = 32
+DECODE_ONE_STREAM = 512
 BEAM_TILE128 = 64
 BEAM_FAST = 256
 TRAIN_BF16 = 128

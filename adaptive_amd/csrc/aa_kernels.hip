@@ -3265,7 +3265,8 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
     return (int)e;
   }
   rc = greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, nullptr, flags, p->cap,
-                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl, p->aux);
+                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl,
+                   (flags & AA_DECODE_ONE_STREAM) ? nullptr : p->aux);
   e = hipStreamEndCapture(p->cap, &p->graph);
   if (rc == 0 && e != hipSuccess) rc = (int)e;
   if (rc == 0) {

@@ -88,6 +88,8 @@ class DecodePipeline:
             slot.aux.wait_event(ready)
         images.record_stream(s)
         flags = m._decode_flags()  # the same flags sampler() passes (fp32_encoder included)
+        if self.graph and not m.split_lstm:  # a plan's side-stream branch would take one more queue
+            flags |= _lib.DECODE_ONE_STREAM
         with torch.cuda.device(dev), torch.cuda.stream(s):
             key = (images.data_ptr(), B, T, m._packed.data_ptr(), flags)
             plan = slot.plans.get(key) if self.graph else None

@@ -222,6 +222,8 @@ def main():
                     "buffer (MALL-resident; not the metric)")
     ap.add_argument("--replicate-buffer", action="store_true", help="diagnostics: distinct feature buffers holding "
                     "copies of the same batch (not the metric)")
+    ap.add_argument("--pipeline-graph", action="store_true", help="pipeline slots replay captured one-stream "
+                    "decode plans (hipGraph) instead of launching kernels directly")
     ap.add_argument("--pool-streams", action="store_true", help="pipeline slots on torch pool streams instead of "
                     "freshly created HIP streams")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
@@ -283,7 +285,8 @@ def main():
                                          graph=not args.no_graph)
         finish(i, ids)
 
-    pipe = DecodePipeline(model, max_len=T, depth=depth, raw_streams=not args.pool_streams)
+    pipe = DecodePipeline(model, max_len=T, depth=depth, raw_streams=not args.pool_streams,
+                          graph=args.pipeline_graph)
 
     def pipelined(n):
         for i, (ids, _, _) in enumerate(pipe.run(bufs[i % nbuf] for i in range(n))):

@@ -190,6 +190,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 #define AA_DECODE_LISTS 32 /* greedy: the vocab screen appends per-row candidate lists against a running max
                              lower bound (k_vscreen3) and k_vrescore3 rescores them, instead of granule
                              summaries (k_vscreen2) + k_vrescore; same ids (measured slower at B = 512) */
+#define AA_DECODE_ONE_STREAM 512 /* decode plans: capture the whole decode on one stream (no side-stream
+                                     branch for the encoder's a_g work); for several plans in flight */
 #define AA_DECODE_ENC_V3 16 /* V on the 128 x 128-tile bf16x3 kernel (k_enc_v3) instead of k_enc_v4 (one
                                workgroup per two images, all H columns; H in {256, 512}) */
 
