@@ -1914,31 +1914,38 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
                                              bf16x8 (*Ws)[SC2_STAGE], float* un_s, floatx16 (&acc)[SC2_NB]) {
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  // this wave's u fragments (row block m0 / 32 + wave) arrive one stage ahead, like the W stage:
-  // a two-stage register ring instead of all KC chunks at once, so the kernel fits in 256 registers
-  // (two waves per SIMD) and 40 KB of LDS -- two workgroups per CU, one per batch in flight
+  // this wave's u fragments (row block m0 / 32 + wave) and the W stages arrive AA_SCREEN_AHEAD stages
+  // ahead in register rings instead of all KC chunks at once, so the kernel fits in 256 registers and
+  // 40 KB of LDS.  Two stages ahead (the default) hide more of the L2 latency than one (k_vscreen2
+  // 16.4 -> 15.5 us in A/B); three cost more in registers than they hide.
   const bf16x8* a0 = ua + (size_t)((m0 >> 5) + wave) * KC * 64 + lane;
-  bf16x8 fa[2][SC2_KS];
+#ifndef AA_SCREEN_AHEAD
+#define AA_SCREEN_AHEAD 2
+#endif
+  // stages in flight ahead of the one multiplied: W in registers (RW slots), u fragments (RU slots)
+  constexpr int AH = AA_SCREEN_AHEAD < NS ? AA_SCREEN_AHEAD : NS, RW = AH, RU = AH + 1;
+  bf16x8 fa[RU][SC2_KS];
   auto uload = [&](int s, int slot) {
 #pragma unroll
     for (int c = 0; c < SC2_KS; ++c) fa[slot][c] = a0[(size_t)(s * SC2_KS + c) * 64];
   };
-  uload(0, 0);
   // W stage s: for column block b (0..4), chunks [s KS, (s+1) KS) are one contiguous 8 KB run of the
   // fragment-order W_m; thread t moves bf16x8 j = t + 256 i of the stage (b = j / (KS*64)).
   const bf16x8* wbase = wf + (size_t)(n0 >> 5) * KC * 64;
-  bf16x8 wr[PER];
-  auto gload = [&](int s) {
+  bf16x8 wr[RW][PER];
+  auto gload = [&](int s, int slot) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int j = t + 256 * i, b = j / (SC2_KS * 64), r = j - b * (SC2_KS * 64);
-      wr[i] = wbase[((size_t)b * KC + s * SC2_KS) * 64 + r];
+      wr[slot][i] = wbase[((size_t)b * KC + s * SC2_KS) * 64 + r];
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, int slot) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) Ws[buf][t + 256 * i] = wr[i];
+    for (int i = 0; i < PER; ++i) Ws[buf][t + 256 * i] = wr[slot][i];
   };
+#pragma unroll
+  for (int s = 0; s < AH; ++s) uload(s, s);
   // epilogue operand, loaded behind the fragments
   if (t < SC2_BM) {
     const int r = m0 + t;
@@ -1948,13 +1955,14 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
   for (int b = 0; b < SC2_NB; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  gload(0);
+#pragma unroll
+  for (int s = 0; s < AH; ++s) gload(s, s);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    lstore(s & 1);
-    if (s + 1 < NS) {
-      gload(s + 1);
-      uload(s + 1, (s + 1) & 1);
+    lstore(s & 1, s % RW);
+    if (s + AH < NS) {
+      gload(s + AH, s % RW);
+      uload(s + AH, (s + AH) % RU);
     }
     __syncthreads();
     const bf16x8* ws = Ws[s & 1] + lane;
@@ -1963,7 +1971,7 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
 #pragma unroll
       for (int b = 0; b < SC2_NB; ++b) {
         const bf16x8 w = ws[(b * SC2_KS + c) * 64];
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][c], w, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s % RU][c], w, acc[b], 0, 0, 0);
       }
     }
   }
