@@ -511,16 +511,25 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
         bf16x8 fa[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(Ab + q * PL + rb * 16 * E4_LD);
-#pragma unroll
-        for (int c = 2 * cp; c < 2 * cp + 2; ++c) {
-          floatx4 x = acc[rb][c];
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c][0], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][1], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][2], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c][0], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][1], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c][0], x, 0, 0, 0);
-          acc[rb][c] = x;
+        // the pair's two accumulator chains interleaved (each chain's product order unchanged:
+        // bit-identical), so no MFMA waits on its immediate predecessor
+        {
+          const int c0 = 2 * cp, c1 = c0 + 1;
+          floatx4 x = acc[rb][c0], y = acc[rb][c1];
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c1][0], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][1], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][1], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][2], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][2], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][0], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][1], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][1], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][0], y, 0, 0, 0);
+          acc[rb][c0] = x;
+          acc[rb][c1] = y;
         }
       }
       gload_w(s1, 2 * cp);
