@@ -70,8 +70,10 @@ class DecodePipeline:
         return self._slots[self._n % self.depth]
 
     @torch.no_grad()
-    def submit(self, images: torch.Tensor) -> None:
-        """Queue one batch (post-trunk features, or images when the model has the trunk)."""
+    def submit(self, images: torch.Tensor, ids_host: torch.Tensor = None) -> None:
+        """Queue one batch (post-trunk features, or images when the model has the trunk).
+        ``ids_host``: a pinned host tensor [B, T] int64 that receives the batch's ids by a copy on the
+        slot's own stream, as the batch's last operation (no work for the caller's stream)."""
         m = self.model
         if len(self._pending) >= self.depth:
             raise RuntimeError("pipeline full: retire() a result first")
@@ -117,6 +119,8 @@ class DecodePipeline:
                                               slot.aux.cuda_stream if m.split_lstm else None)
                 _lib.check(rc, "greedy_decode")
                 out = (ids, alpha, beta)
+            if ids_host is not None:
+                ids_host.copy_(out[0], non_blocking=True)
             done = torch.cuda.Event()
             done.record(s)
         self._pending.append((done, out, images))
@@ -131,10 +135,13 @@ class DecodePipeline:
             t.record_stream(cur)
         return out
 
-    def run(self, batches: Iterable[torch.Tensor]) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
-        for images in batches:
+    def run(self, batches: Iterable[torch.Tensor], ids_host=None) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        """``ids_host``: optional list of pinned host tensors, used round-robin per submitted batch
+        (see ``submit``); a buffer is reused only after its batch was retired when the list holds
+        more than ``depth`` buffers."""
+        for i, images in enumerate(batches):
             if len(self._pending) >= self.depth:
                 yield self.retire()
-            self.submit(images)
+            self.submit(images, None if ids_host is None else ids_host[i % len(ids_host)])
         while self._pending:
             yield self.retire()

@@ -271,6 +271,9 @@ def main():
         for b_ in bufs[1:]:
             b_.copy_(feats)
     host_ids = [torch.empty(world * B, T, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+    # one-GPU pipelined region: each batch's ids leave on its own slot stream (DecodePipeline(ids_host)),
+    # so the caller's stream carries no copies between the slots' batches
+    pipe_host = [torch.empty(B, T, dtype=torch.int64, pin_memory=True) for _ in range(depth + 1)]
 
     def finish(i, ids):
         """The step's tail inside the timed region: for N > 1 the one all-gather of token ids
@@ -289,13 +292,20 @@ def main():
                           graph=args.pipeline_graph)
 
     def pipelined(n):
+        if world == 1 and not args.no_d2h:
+            for _ in pipe.run((bufs[i % nbuf] for i in range(n)), ids_host=pipe_host):
+                pass
+            return
         for i, (ids, _, _) in enumerate(pipe.run(bufs[i % nbuf] for i in range(n))):
             finish(i, ids)
 
-    for i in range(max(args.warmup, 3 * nbuf)):  # every buffer seen twice: its decode plan is captured
-        step(i)
-    pipelined(max(args.warmup, 2 * depth + 1))
     K = args.steps
+    # untimed warm-up: every buffer seen twice (its decode plan is captured), then one region's worth
+    # of sequential steps and four of pipelined batches (the first pipelined regions otherwise ran 5-10 %
+    # low, settling after ~150 batches)
+    for i in range(max(args.warmup, 3 * nbuf, K)):
+        step(i)
+    pipelined(max(args.warmup, 2 * depth + 1, 4 * K))
     traces = []
     if not args.no_trace:
         for _ in range(K):
