@@ -1914,6 +1914,83 @@ __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0,
   }
 }
 
+// screen_block_summ over a wave's NB column blocks at once, each butterfly level issued for every
+// block before the next level starts: with one wave per SIMD (k_vscreen2's grid is one workgroup
+// per CU) the late levels of one block (1 or 2 independent merges) leave the SIMD waiting on DPP and
+// VALU latency; NB blocks side by side give each level NB times the independent work.  The top-2
+// merge is max / med3: the second largest of {m1 >= m2, r1 >= r2} is med3(m1, r1, max(m2, r2)).
+// Same keys, same summaries as screen_block_summ per block.
+// median of three (the compiler emits v_med3_u32 for this pattern)
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+  const uint32_t t = hi < c ? hi : c;
+  return lo > t ? lo : t;
+}
+
+template <int M>
+__device__ __forceinline__ void screen_bfly_m3(uint32_t (&k1)[16], uint32_t (&k2)[16], int li) {
+  const bool hi = (li & M) != 0;
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    const uint32_t s1 = hi ? k1[k] : k1[k + M / 2], s2 = hi ? k2[k] : k2[k + M / 2];
+    const uint32_t m1 = hi ? k1[k + M / 2] : k1[k], m2 = hi ? k2[k + M / 2] : k2[k];
+    const uint32_t r1 = partner<M>(s1), r2 = partner<M>(s2);
+    const uint32_t h2 = m2 > r2 ? m2 : r2;
+    k1[k] = m1 > r1 ? m1 : r1;
+    k2[k] = umed3(m1, r1, h2);
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], int row0, int G0, const float (&bv)[NB],
+                                                   const float2* __restrict__ gs, const float* __restrict__ un_blk,
+                                                   int c0, int V, int B, int NTn, float4* __restrict__ summ) {
+  const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  uint32_t k1[NB][16], k2[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const bool valid = c0 + 32 * b + li < V;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t key = order_key(acc[b][r] + bv[b]);
+      k1[b][r] = valid ? (key & ~31u) | (uint32_t)li : 0u;
+      k2[b][r] = 0u;
+    }
+  }
+  // level 16 keeps a block's 16 keys live until it is done: block by block (8 independent merges each)
+#pragma unroll
+  for (int b = 0; b < NB; ++b) screen_bfly_m3<16>(k1[b], k2[b], li);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) screen_bfly_m3<8>(k1[b], k2[b], li);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) screen_bfly_m3<4>(k1[b], k2[b], li);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) screen_bfly_m3<2>(k1[b], k2[b], li);
+  const int rr = (li >> 1) & 15;  // this lane pair now holds row acc_row(rr) of each block
+  const int rl = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+  const int row = row0 + rl;
+  const float uw0 = un_blk[rl];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint32_t r1 = partner<1>(k1[b][0]), r2 = partner<1>(k2[b][0]);
+    const uint32_t m1 = k1[b][0] > r1 ? k1[b][0] : r1;
+    const uint32_t h2 = k2[b][0] > r2 ? k2[b][0] : r2;
+    const uint32_t m2 = umed3(k1[b][0], r1, h2);
+    if (!(li & 1) && row < B) {
+      float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+      if (m1) {
+        const float2 gsv = gs[G0 + b];
+        const float uw = uw0 * gsv.x;
+        const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+        const float x1 = key_value(m1 & ~31u);
+        const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
+        o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + b) * VS_TILE + (int)(m1 & 31u)));
+      }
+      summ[(int64_t)row * NTn + G0 + b] = o;
+    }
+  }
+}
+
 // Main loop of the wide screen (k_vscreen2 / k_vscreen3): the tile's screened products
 // acc[b] = bf16(u) . bf16(w) of wave w's 32 rows x column block b (no bias), and un_s = ||u|| of the
 // tile's 128 rows.
@@ -2006,11 +2083,18 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
   screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc);
   AA_TS(2, 1);
   const int row0 = m0 + 32 * wave;
+#ifndef AA_SCREEN_EPI
+#define AA_SCREEN_EPI 1
+#endif
+#if AA_SCREEN_EPI
+  screen_blocks_summ<SC2_NB>(acc, row0, n0 / VS_TILE, bvs, gs, un_s + 32 * wave, n0, V, B, NTn, summ);
+#else
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b) {
     const int G = n0 / VS_TILE + b;
     screen_block_summ(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
   }
+#endif
   AA_TS(2, 2);
 }
 
