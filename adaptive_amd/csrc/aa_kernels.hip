@@ -2136,7 +2136,9 @@ __device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, co
 // one granule).  32 candidates are scored per pass (8 lanes each, exact_logit8); first-index argmax
 // -> keys[row], ids[row, t].  A list longer than RS_CAP falls back to every column (correct, slow).
 // (Tried: re-screening a ub2 >= M granule's 32 columns in bf16 here, sequentially or 64 columns per
-// round, and scoring only those within the bound: fewer exact logits, but slower overall.)
+// round, and scoring only those within the bound: fewer exact logits, but slower overall.  Also
+// tried: each wave reading the W row of its best granule's arg-max column before the barriers, as a
+// cache warm-up for the likely winner: k_vrescore 9.95 -> 10.4 us by events in A/B.)
 // ---------------------------------------------------------------------------------------------
 #ifndef AA_RS_THREADS
 #define AA_RS_THREADS 256
