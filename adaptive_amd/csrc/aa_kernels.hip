@@ -1941,6 +1941,19 @@ __device__ __forceinline__ void screen_bfly_m3(uint32_t (&k1)[16], uint32_t (&k2
   }
 }
 
+// First level (M = 16, every k2 still 0) by v_permlane16_swap (gfx950): swapping the odd 16-lane
+// rows of k1[k] with the even rows of k1[k + 8] leaves each lane holding its own key and its
+// partner's (lane ^ 16) for exactly the row it keeps (k on the low half, k + 8 on the high half),
+// so the level needs no selects and no ds_swizzle; top-2 of two keys = max / min.
+__device__ __forceinline__ void screen_bfly16_swap(uint32_t (&k1)[16], uint32_t (&k2)[16]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const auto r = __builtin_amdgcn_permlane16_swap(k1[k], k1[k + 8], false, false);
+    k1[k] = r[0] > r[1] ? r[0] : r[1];
+    k2[k] = r[0] > r[1] ? r[1] : r[0];
+  }
+}
+
 template <int NB>
 __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], int row0, int G0, const float (&bv)[NB],
                                                    const float2* __restrict__ gs, const float* __restrict__ un_blk,
@@ -1957,9 +1970,8 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
       k2[b][r] = 0u;
     }
   }
-  // level 16 keeps a block's 16 keys live until it is done: block by block (8 independent merges each)
 #pragma unroll
-  for (int b = 0; b < NB; ++b) screen_bfly_m3<16>(k1[b], k2[b], li);
+  for (int b = 0; b < NB; ++b) screen_bfly16_swap(k1[b], k2[b]);
 #pragma unroll
   for (int b = 0; b < NB; ++b) screen_bfly_m3<8>(k1[b], k2[b], li);
 #pragma unroll
