@@ -354,7 +354,7 @@ class Encoder2Decoder(nn.Module):
         if self.distributed_sampler and trace is None:
             import torch.distributed as dist
             if dist.is_initialized() and dist.get_world_size() > 1:
-                return self.sharded_sampler(images, max_len)
+                return self.sharded_sampler(images, max_len, exact_vocab=exact_vocab, lanes=lanes, graph=graph)
         return self._sampler_local(images, max_len, trace, exact_vocab, lanes, graph)
 
     @torch.no_grad()
@@ -409,7 +409,8 @@ class Encoder2Decoder(nn.Module):
 
     @torch.no_grad()
     def sharded_sampler(self, images: torch.Tensor, max_len: int = 30, total: Optional[int] = None, group=None,
-                        gather_attention: bool = True):
+                        gather_attention: bool = True, exact_vocab: bool = False, lanes: Optional[int] = None,
+                        graph: Optional[bool] = None):
         """Multi-rank ``sampler``: the one-process-per-GPU counterpart of the reference's
         self-distributing sampler (``nn.DataParallel`` over every visible GPU,
         adaptive_attention.py:178-181).  Every rank of ``group`` (``torch.distributed``; ``nccl`` =
@@ -418,7 +419,8 @@ class Encoder2Decoder(nn.Module):
         returns the whole batch's results on every rank -- the same values as one ``sampler`` call
         over all rows (rows never interact, and no kernel's per-row arithmetic depends on the batch
         size).  ``images``: the full batch on every rank (``total=None``), or this rank's block of a
-        ``total``-row batch."""
+        ``total``-row batch.  ``exact_vocab``, ``lanes`` and ``graph`` apply to each rank's local
+        decode as in ``sampler``."""
         import torch.distributed as dist
         from . import distributed as D
         if not dist.is_initialized():
@@ -426,7 +428,10 @@ class Encoder2Decoder(nn.Module):
         if total is None:
             total = images.size(0)
             images = D.local_rows(images, group)
-        ids, alpha, beta = D.sharded_sampler(lambda x, t: self._sampler_local(x, t), images, int(total), int(max_len),
+        def local(x, t):
+            return self._sampler_local(x, t, exact_vocab=exact_vocab, lanes=lanes, graph=graph)
+
+        ids, alpha, beta = D.sharded_sampler(local, images, int(total), int(max_len),
                                              group=group, gather_attention=gather_attention)
         return ids, alpha, beta
 
@@ -477,11 +482,14 @@ class Encoder2Decoder(nn.Module):
         return ids, alpha, beta, seqs, scores
 
     def _aux_stream(self, dev) -> torch.cuda.Stream:
-        """The side stream of ``aa_greedy_decode_aux`` on ``dev`` (created once, reused)."""
+        """The side stream of ``aa_greedy_decode_aux`` on ``dev`` (created once, reused): a fresh HIP
+        stream (hip_events.new_raw_stream), so it takes its own hardware queue in HIP's round-robin
+        instead of a torch pool stream whose queue may be the caller's."""
         cache = self.__dict__.setdefault("_aux_streams", {})
         key = dev.index if dev.index is not None else torch.cuda.current_device()
         if key not in cache:
-            cache[key] = torch.cuda.Stream(device=dev)
+            from .hip_events import new_raw_stream
+            cache[key] = new_raw_stream(dev)
         return cache[key]
 
     def _train_flags(self) -> int:
@@ -496,12 +504,13 @@ class Encoder2Decoder(nn.Module):
                 | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0) | (_lib.DECODE_LISTS if self.vocab_lists else 0))
 
     def _lanes(self, n: int, dev) -> list:
-        """n side streams on ``dev`` (created once, reused)."""
+        """n side streams on ``dev`` (created once, reused; fresh HIP streams, as ``_aux_stream``)."""
+        from .hip_events import new_raw_stream
         cache = self.__dict__.setdefault("_lane_streams", {})
         key = (dev.index if dev.index is not None else torch.cuda.current_device())
         have = cache.setdefault(key, [])
         while len(have) < n:
-            have.append(torch.cuda.Stream(device=dev))
+            have.append(new_raw_stream(dev))
         return have[:n]
 
     def _workspace(self, nbytes: int, dev) -> Optional[torch.Tensor]:

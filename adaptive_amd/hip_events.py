@@ -80,23 +80,42 @@ class EventArray:
 
 
 _raw_streams = {}
+_owned_streams = []  # streams handed out by new_raw_stream (kept alive for the process)
+
+
+def _create(idx: int) -> "torch.cuda.ExternalStream":
+    h = c_void_p()
+    with torch.cuda.device(idx):
+        rc = hip().hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
+    if rc != 0:
+        raise RuntimeError(f"hipStreamCreateWithFlags failed: {rc}")
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+
+
+def _index(device) -> int:
+    dev = torch.device(device)
+    return dev.index if dev.index is not None else torch.cuda.current_device()
 
 
 def raw_streams(device, n: int):
-    """The first ``n`` of this process's fresh non-blocking HIP streams on ``device``
+    """The first ``n`` of this process's SHARED fresh non-blocking HIP streams on ``device``
     (hipStreamCreateWithFlags), as torch.cuda.ExternalStream objects.  HIP assigns each new stream a
     hardware queue round-robin (GPU_MAX_HW_QUEUES, 4 by default), so streams created back to back land
     on distinct queues -- unlike streams handed out by torch's pool, whose queues were fixed when the
     pool was made.  They live as long as the process (torch's caching allocator may still record
-    events on them after their user is gone), and are reused by later callers."""
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    events on them after their user is gone), and every caller gets the same first ``n``: two users
+    of this list serialise against each other on the streams they share."""
+    idx = _index(device)
     have = _raw_streams.setdefault(idx, [])
     while len(have) < n:
-        h = c_void_p()
-        with torch.cuda.device(idx):
-            rc = hip().hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
-        if rc != 0:
-            raise RuntimeError(f"hipStreamCreateWithFlags failed: {rc}")
-        have.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx)))
+        have.append(_create(idx))
     return have[:n]
+
+
+def new_raw_stream(device) -> "torch.cuda.ExternalStream":
+    """A fresh non-blocking HIP stream on ``device`` that no other caller of this module gets (it
+    takes the next hardware queue in HIP's round-robin at the time of the call).  Kept alive for the
+    process, as ``raw_streams``."""
+    st = _create(_index(device))
+    _owned_streams.append(st)
+    return st

@@ -34,8 +34,22 @@ class _Slot:
         """The slot's side stream (aa_greedy_decode_aux's split LSTM steps), made on first use only:
         an unused stream still takes a hardware queue in HIP's round-robin assignment."""
         if self._aux is None:
-            self._aux = torch.cuda.Stream(device=self.dev)
+            from .hip_events import new_raw_stream
+            self._aux = new_raw_stream(self.dev)
         return self._aux
+
+
+class Retired(tuple):
+    """One retired batch: unpacks as ``(ids, alpha, beta)``; ``.done`` is the batch's completion
+    event (recorded on its slot stream, after its ids host copy) and ``.ids_host`` the pinned host
+    tensor its ids were copied into (None without ``ids_host``).  The host tensor may be read only
+    after ``.done`` has completed -- ``done.synchronize()``, or a synchronisation of the caller's
+    stream, which ``retire`` made wait on it."""
+
+    def __new__(cls, out, done, ids_host):
+        r = super().__new__(cls, out)
+        r.done, r.ids_host = done, ids_host
+        return r
 
 
 class DecodePipeline:
@@ -46,7 +60,12 @@ class DecodePipeline:
     process then owns exactly ``depth`` busy streams.  HIP multiplexes a process's streams onto a
     few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and two slots that land on one queue
     serialise; captured plans (``graph=True``) add the graph executor's own branch streams to that
-    count, which made the overlap hit-or-miss in measurements."""
+    count, which made the overlap hit-or-miss in measurements.
+
+    With ``raw_streams=True`` (default) the slots use the first ``depth`` of the process-wide list of
+    fresh HIP streams (``hip_events.raw_streams``): two pipelines alive on one device share those
+    streams and therefore serialise against each other (results stay correct; only their overlap is
+    lost)."""
 
     MAX_PLANS = 2
 
@@ -123,22 +142,24 @@ class DecodePipeline:
                 ids_host.copy_(out[0], non_blocking=True)
             done = torch.cuda.Event()
             done.record(s)
-        self._pending.append((done, out, images))
+        self._pending.append((done, out, images, ids_host))
         self._n += 1
 
-    def retire(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """The oldest queued batch's (ids, alpha, beta); the caller's stream waits for it."""
-        done, out, _ = self._pending.popleft()
+    def retire(self) -> "Retired":
+        """The oldest queued batch's (ids, alpha, beta) as a ``Retired`` tuple; the caller's stream
+        waits for it (the host is not synchronised: read ``ids_host`` only after ``.done``)."""
+        done, out, _, ids_host = self._pending.popleft()
         cur = torch.cuda.current_stream()
         cur.wait_event(done)
         for t in out:
             t.record_stream(cur)
-        return out
+        return Retired(out, done, ids_host)
 
     def run(self, batches: Iterable[torch.Tensor], ids_host=None) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
         """``ids_host``: optional list of pinned host tensors, used round-robin per submitted batch
-        (see ``submit``); a buffer is reused only after its batch was retired when the list holds
-        more than ``depth`` buffers."""
+        (see ``submit``); a buffer is handed to a new batch only after its previous batch was
+        retired when the list holds more than ``depth`` buffers.  Each yielded ``Retired`` names its
+        buffer (``.ids_host``), readable once ``.done`` has completed."""
         for i, images in enumerate(batches):
             if len(self._pending) >= self.depth:
                 yield self.retire()

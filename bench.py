@@ -4,19 +4,28 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 512] [--max-len 20]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
+``--gpus N`` with N > 1 and no torchrun environment (WORLD_SIZE unset) starts the N ranks itself:
+torch.distributed.run as a CHILD process (never an exec), before any GPU call, whose rank 0 prints
+the line; the exit code is the child's.  (The reference's sampler distributes itself over every
+visible GPU with no launcher, code_src/models/adaptive_attention.py:178-181.)
+
 A "step" = one sampler() call over this rank's B = 512 synthetic images (post-trunk features
 [B,2048,7,7], U[0,1), counter-based; random-init weights of the reference architecture, seed 123)
 plus, for N > 1, the RCCL all-gather of the token ids (the path's only collective,
 adaptive_amd.distributed.gather_rows), plus the ids device -> host copy.  Each rank
 decodes its own rows (weak scaling: global batch = 512 N).  Inputs are resident in HBM before the
-timed region, one distinct feature batch per batch in flight.  Every mode is timed over >= 5
-regions of exactly K steps and the median region is reported.  Rank 0 prints ONE JSON line.
+timed region.  ``value`` is SURVEY.md §8d's metric: captions / median wall time of one sampler()
+call after another (the reference's eval loop, code_src/tools/utils.py:167-171).  The same K
+batches with several in flight (adaptive_amd.pipeline.DecodePipeline, one distinct feature batch
+per batch in flight) are reported in ``pipelined``.  Every mode is timed over >= 5 regions of
+exactly K steps and the median region is reported.  Rank 0 prints ONE JSON line.
 
-Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic FLOPs / its average
-HIP-event duration inside a traced region), ``kernels`` (all per-kernel averages),
-``path_roofline`` (every kernel's executed work at its own ceiling, summed, over the measured time
-per batch), ``cpu_baseline`` (the PyTorch-CPU restatement of the reference sampler,
-oracle/adaptive_oracle.py, timed on this host's cores, rank 0, N=1).
+Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic bytes or FLOPs / its
+average HIP-event duration inside a traced region), ``kernels`` (all per-kernel averages),
+``hbm_frac_path`` (§8d: bytes(B) per step / step time / 8 TB/s), ``fp32_binding`` (§8d's binding
+figure F x captions/s / 157.3 TF), ``path_roofline`` (every kernel's work at its own ceiling,
+summed, over the measured time per batch), ``cpu_baseline`` (the PyTorch-CPU restatement of the
+reference sampler, oracle/adaptive_oracle.py, timed on this host's cores, rank 0, N=1).
 """
 from __future__ import annotations
 
@@ -172,24 +181,100 @@ def cpu_baseline(feats_cpu: torch.Tensor, T: int, budget_s: float) -> dict:
             "cpus": cpus}
 
 
-def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True) -> dict:
-    """Executed work of one decode priced at each kernel's own ceiling: bf16x3 GEMMs
-    at bf16 peak / 6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen (all Vp padded
-    columns) at the bf16 peak, the attention and rescoring at HBM peak for their bytes.  The sum is
-    the time a decode would take if every kernel ran at its roofline, back to back."""
+def path_bytes(B: int, T: int) -> int:
+    """SURVEY.md §8d's ALGORITHMIC bytes per batch: inputs + outputs per caption, every weight once,
+    the embedding rows the tokens touch (268.5 MB at B = 512, T = 20).  The input term counts the
+    [B,49,2048] map and a_g [B,2048] as §8d does (409,600 B per caption); per-step re-reads of V are
+    not algorithmic bytes."""
+    return B * (C * (P + 1) * 4 + T * (8 + 4 * P + 4)) + 46_263_024 + min(B * T, V) * E * 4
+
+
+def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True, v_restream: bool = True) -> dict:
+    """Work of one decode priced at each kernel's own ceiling: bf16x3 GEMMs at bf16
+    peak / 6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen (all Vp padded columns) at the
+    bf16 peak, the attention and rescoring at HBM peak for their bytes.  The sum is the time a decode
+    would take if every kernel ran at its roofline, back to back.  ``v_restream=False`` leaves the
+    attention's per-step re-read of V out of its bytes (§8d: not algorithmic; V is produced once by
+    the encoder), which is the ideal the path is graded against."""
     f = flops_per_caption(T)
+    atten_row = atten_bytes_per_row() - (0 if v_restream else 4 * P * H)
     parts = {
         "k_enc_v4": f["k_enc_v"] * B / PEAK_X3,
         "k_enc_heads3": f["k_enc_heads"] * B / PEAK_X3,
         "k_gemm_bias(VWv)": f["vwv"] * B / PEAK_FP32,
         "k_gemm_bias(x_g)": f["xg"] * B / PEAK_FP32,
         "k_lstm": T * (f["k_lstm_gemm"] * B / PEAK_X3 + f["proj"] * B / PEAK_FP32),
-        "k_atten": T * atten_bytes_per_row() * B / PEAK_HBM,
+        "k_atten": T * atten_row * B / PEAK_HBM,
         "k_vscreen": T * 2 * H * Vp * B / PEAK_BF16,
     }
     rescore = "k_vrescore3" if lists else "k_vrescore"
     parts[rescore] = T * kernel_costs(B, T)[rescore][1] / PEAK_HBM
     return {"total": sum(parts.values()), "parts": parts}
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """Start ``n`` ranks of this script under torch.distributed.run as a child process (one process
+    per GPU, rendezvous on 127.0.0.1) and return its exit code.  Called before anything touches the
+    GPU.  The ranks' stdout is forwarded line by line as it arrives: the JSON line (rank 0's) to this
+    process's stdout, anything else the ranks' libraries print there (e.g. gloo's connection notes)
+    to stderr, so stdout carries exactly the one line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box's driver supports dmabuf IPC only
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    log(f"starting {n} ranks: {' '.join(cmd[1:])}")
+    with subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1) as p:
+        for line in p.stdout:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+        return p.wait()
+
+
+def time_region(run, world: int, sync, dev) -> float:
+    """Wall time of ``run()`` bracketed by barrier + device synchronisation on both sides, max over
+    ranks (the whole job ends when its slowest rank does)."""
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    return el
+
+
+def plumbing_main(args, world: int, rank: int) -> None:
+    """``--cpu-plumbing``: the N > 1 launch path without a GPU (CPU tests): gloo ranks, the ids
+    all-gather of a stand-in [B, T] shard through adaptive_amd.distributed.gather_rows, timed regions
+    with max-over-ranks, one JSON line from rank 0.  Measures nothing about the decode."""
+    dist.init_process_group("gloo")
+    B, T = args.batch, args.max_len
+    dev = torch.device("cpu")
+    ids = torch.arange(rank * B * T, (rank + 1) * B * T, dtype=torch.int64).view(B, T)
+    got = []
+
+    def run():
+        got.append(gather_rows(ids, world * B))
+
+    regions = [time_region(run, world, lambda: None, dev) for _ in range(max(5, args.regions))]
+    ok = all(torch.equal(g, torch.arange(world * B * T, dtype=torch.int64).view(world * B, T)) for g in got)
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing rehearsal (no GPU, no decode)", "value": None, "n_gpus": world,
+                          "ranks_seen": dist.get_world_size(), "backend": dist.get_backend(),
+                          "gathered_ok": ok, "regions_s": regions}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
@@ -228,14 +313,21 @@ def main():
                     "freshly created HIP streams")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--cpu-plumbing", action="store_true", help="CPU tests only: run the N > 1 launch / gather / "
+                    "timing path over gloo with no GPU and no decode (prints a plumbing line, not the metric)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver runs `python bench.py --gpus N`: start the N ranks here (child process, no GPU touched yet)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit(f"--gpus {args.gpus} needs a torchrun launch with {args.gpus} processes")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.cpu_plumbing:
+        plumbing_main(args, world, rank)
+        return
     # AA_DIST_BACKEND=gloo: rehearsal of the N > 1 path with several ranks sharing the visible GPUs
     # (ids gathered through the host; not a scaling measurement)
     backend = os.environ.get("AA_DIST_BACKEND", "nccl")
@@ -316,38 +408,27 @@ def main():
             traces.append((ev, tr))
 
     def timed(trace_list, pipeline=False):
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if pipeline:
-            pipelined(K)
-        else:
-            for k in range(K):
-                step(k, trace_list[k][1] if trace_list else None)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
-        return el
+        def run():
+            if pipeline:
+                pipelined(K)
+            else:
+                for k in range(K):
+                    step(k, trace_list[k][1] if trace_list else None)
+        return time_region(run, world, torch.cuda.synchronize, dev)
 
     # Regions: `--regions` (>= 5) timed regions of exactly K steps each for the sequential sampler
-    # calls and, when depth > 1, for DecodePipeline (the headline); value = the median region.  Then
-    # one more region of the K sequential steps with a HIP event pair around every kernel launch
-    # (on its launch stream) for the per-kernel averages; events are timestamp packets in the queue,
-    # so that region runs a little slower and is reported separately as ``traced_ms_per_step``.
+    # calls (the headline) and, when depth > 1, for DecodePipeline (``pipelined``);
+    # each mode reports its median region.  Then one more region of the K sequential steps with a HIP
+    # event pair around every kernel launch (on its launch stream) for the per-kernel averages;
+    # events are timestamp packets in the queue, so that region runs a little slower and is reported
+    # separately as ``traced_ms_per_step``.
     R = max(5, args.regions)
     seq_regions = [timed(None) for _ in range(R)]
     log(f"sequential regions (s): {seq_regions}")
     pipe_regions = [timed(None, pipeline=True) for _ in range(R)] if depth > 1 else seq_regions
     log(f"pipelined regions (s): {pipe_regions}")
-    elapsed_seq = float(np.median(seq_regions))
-    elapsed = float(np.median(pipe_regions))
+    elapsed = float(np.median(seq_regions))
+    elapsed_pipe = float(np.median(pipe_regions))
     traced_elapsed = timed(traces) if traces else None
     captions = world * B * K
     value = captions / elapsed
@@ -414,7 +495,10 @@ def main():
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"]}
 
-    ideal = path_ideal_seconds(B, T, lists=lists)
+    ideal = path_ideal_seconds(B, T, lists=lists, v_restream=False)
+    ideal_exec = path_ideal_seconds(B, T, lists=lists, v_restream=True)
+    F = flops_per_caption(T)["total"]
+    per_gpu_rate, per_gpu_rate_pipe = value / world, captions / elapsed_pipe / world
     out = {
         "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -426,29 +510,53 @@ def main():
                    "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else "")
                    + ("" if backend == "nccl" else f" ({backend} rehearsal)"),
                    "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
-                   "batches_in_flight": depth, "feature_buffers": nbuf,
-                   # how each region launches: the pipeline's slots launch kernels directly (its
-                   # graph=False default); the sequential region replays captured decode plans
-                   "hip_graph": {"pipelined": pipe.graph, "sequential": not args.no_graph},
+                   "batches_in_flight": 1, "feature_buffers": nbuf,
+                   # how each region launches: the headline's sampler() calls replay captured decode
+                   # plans; the pipeline's slots launch kernels directly (its graph=False default)
+                   "hip_graph": {"sequential": not args.no_graph, "pipelined": pipe.graph},
                    "vocab_stage": "k_vscreen3 (screen + per-row candidate lists) + k_vrescore3" if lists
                    else "k_vscreen2/k_vscreen (granule summaries) + k_vrescore",
                    "lstm_step": "split (k_lstm_gemm on a side stream + k_lstm_cell)" if model.split_lstm
                    else "fused (k_lstm)",
-                   "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy"},
-        "regions": {"count": R, "pipelined_captions_per_s": [captions / e for e in pipe_regions],
-                    "sequential_captions_per_s": [captions / e for e in seq_regions], "reported": "median"},
-        "sequential": {"value": captions / elapsed_seq, "ms_per_step": 1e3 * elapsed_seq / K,
-                       "note": "one sampler() call after another (batches_in_flight = 1); SURVEY.md §8d's "
-                               "B / sampler wall-time"},
+                   "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy",
+                   "headline": "one sampler() call after another (the reference's eval loop, utils.py:167-171)"},
+        "ranks_seen": dist.get_world_size() if world > 1 else 1,
+        "backend": (dist.get_backend() if world > 1 else None),
+        "regions": {"count": R, "sequential_captions_per_s": [captions / e for e in seq_regions],
+                    "pipelined_captions_per_s": [captions / e for e in pipe_regions], "reported": "median"},
+        "pipelined": {"value": captions / elapsed_pipe, "ms_per_step": 1e3 * elapsed_pipe / K,
+                      "batches_in_flight": depth, "hip_graph": pipe.graph,
+                      "note": "the same K batches with `batches_in_flight` in flight through "
+                              "adaptive_amd.pipeline.DecodePipeline (each batch its own resident features, "
+                              "its ids copied to the host on its own stream); an API the reference does not call"},
+        # the north star's "fraction of the HBM roofline" -- algorithmic bytes of one step
+        # (inputs + outputs + every weight once + the embedding rows touched) over the step time
+        "hbm_frac_path": path_bytes(B, T) * per_gpu_rate / B / PEAK_HBM,
+        "hbm_frac_path_pipelined": path_bytes(B, T) * per_gpu_rate_pipe / B / PEAK_HBM,
+        "path_bytes_per_batch": path_bytes(B, T),
+        # SURVEY.md §8d's binding figure: F = 415,361,744 FLOP per caption against the fp32 peak
+        "fp32_binding": {"flops_per_caption": F, "achieved_tflops": F * per_gpu_rate / 1e12,
+                         "peak_tflops": PEAK_FP32 / 1e12, "frac": F * per_gpu_rate / PEAK_FP32,
+                         "frac_pipelined": F * per_gpu_rate_pipe / PEAK_FP32,
+                         "note": "F is the pure-fp32 algorithm's FLOP count; this build exceeds the fp32 ceiling "
+                                 "because half of F (the 2HV vocab contraction) runs as a bf16 MFMA screen under a "
+                                 "rigorous error bound with exact fp32 rescoring of the few candidates, and the "
+                                 "encoder and LSTM GEMMs run as fp32-accurate bf16x3 MFMA (6 bf16 products, "
+                                 "2.67x the fp32 MFMA rate); ids stay bit-identical to the fp32 reference"},
         "roofline": roofline,
         "path_roofline": {"bound": "per-kernel", "ideal_ms_per_batch": 1e3 * ideal["total"],
                           "frac": 1e3 * ideal["total"] / ms_per_step,
-                          "frac_sequential": 1e3 * ideal["total"] / (1e3 * elapsed_seq / K),
+                          "frac_pipelined": 1e3 * ideal["total"] / (1e3 * elapsed_pipe / K),
                           "ideal_ms_by_kernel": {k: 1e3 * v for k, v in ideal["parts"].items()},
-                          "note": "executed work of every kernel of one decode at its own ceiling (bf16x3 GEMMs "
-                                  "at bf16 peak/6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen over "
-                                  "all padded columns at the bf16 peak, attention / rescoring bytes at HBM "
-                                  "peak), summed, divided by the measured time per batch of 512"},
+                          "ideal_ms_per_batch_with_v_restream": 1e3 * ideal_exec["total"],
+                          "frac_with_v_restream": 1e3 * ideal_exec["total"] / ms_per_step,
+                          "note": "work of every kernel of one decode at its own ceiling (bf16x3 GEMMs at bf16 "
+                                  "peak/6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen over all padded "
+                                  "columns at the bf16 peak, attention / rescoring bytes at HBM peak), summed, "
+                                  "divided by the measured time per batch; the attention's per-step re-read of V "
+                                  "(51.4 MB per step at B=512) is excluded from `ideal_ms_per_batch` (not "
+                                  "algorithmic bytes, SURVEY.md §8d) and included in the `_with_v_restream` "
+                                  "figures"},
         "kernels": kernels,
         "traced_ms_per_step": None if traced_elapsed is None else 1e3 * traced_elapsed / K,
         "cpu_baseline": None,

@@ -111,7 +111,7 @@ def main():
            "config": {"workload": f"Encoder2Decoder.beam_search B={B} beam={K} max_len={T}", "batch": B,
                       "beam": K, "T": T, "rows": B * K,
                       "vocab_kernel": ("bf16x3 " + ("k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"))
-                      if args.fast else "exact fp32: k_vocab (fp32 MFMA) + k_gsumm summaries",
+                      if args.fast else "exact fp32: k_vexact (fused fp32 MFMA logits + granule summaries)",
                       "mode": "fast (opt-in bf16x3)" if args.fast else "exact (default)"},
            "best_score_mean": float(out[4][:, 0].mean().item()), "roofline": roofline, "cpu_baseline": None}
     if not args.no_cpu_baseline:

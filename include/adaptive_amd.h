@@ -258,7 +258,10 @@ AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
  * workspace; aa_train_backward takes dL/dscores [N][V] with the same arguments and workspace and
  * writes the gradient of every parameter (assigned, not accumulated), and, if dfeats is not NULL,
  * dL/dfeats [B,C,7,7] (the gradient into the ResNet trunk's output, for CNN fine-tuning).  The reference's loss
- * (train.py: CrossEntropyLoss on the packed scores) stays with the caller. */
+ * (train.py: CrossEntropyLoss on the packed scores) stays with the caller.  Token ids are not
+ * validated on the device: the caller must keep them in [0, V) (the Python layer raises IndexError
+ * as nn.Embedding does); an out-of-range id is clamped into [0, V) by the gather (no out-of-bounds
+ * read) and then feeds the wrong embedding row. */
 AA_API size_t aa_train_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
 #define AA_TRAIN_BF16 128 /* aa_train_forward / aa_train_backward flags: every GEMM on bf16 MFMA
                                (operands rounded to bf16, fp32 accumulation; BASELINE config 5's
@@ -282,7 +285,9 @@ AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const
  * (no packing); the sentinel's h_{t-1} is 0 at t = 0 (init_hidden, :116-120).  Outputs (each may be
  * NULL): scores [B,T,V], alpha [B,T,P], beta [B,T], h_out / c_out [B,H] = the states after step
  * T-1.  Forward only (the training path with gradients is aa_train_forward/backward); flags:
- * AA_TRAIN_BF16 or 0 as for aa_train_forward.  Workspace: aa_decoder_workspace_bytes. */
+ * AA_TRAIN_BF16 or 0 as for aa_train_forward.  Workspace: aa_decoder_workspace_bytes.  Token ids:
+ * the caller keeps them in [0, V), as for aa_train_forward (out-of-range ids are clamped, not
+ * reported). */
 AA_API size_t aa_decoder_workspace_bytes(const aa_dims* dims, int32_t B, int32_t T);
 AA_API int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, const float* V, const float* v_g,
                               const float* h0, const float* c0, int32_t B, int32_t T, const int64_t* tokens,

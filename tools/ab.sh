@@ -12,6 +12,6 @@ for rep in 1 2; do
     echo "rep$rep $(basename $lib) $(python -c "
 import json;d=json.load(open('gpurun_out/ab.json'))
 k=' '.join(f'{n}={v[\"avg_ms\"]*1e3:.2f}' for n,v in d['kernels'].items() if n in ('k_lstm','k_atten','k_vscreen','k_vrescore','k_enc_v4'))
-print('pipe', round(d['value']), 'seq', round(d['sequential']['value']), 'ms', round(d['ms_per_step'],4), round(d['sequential']['ms_per_step'],4), k)")"
+print('seq', round(d['value']), 'pipe', round(d['pipelined']['value']), 'ms', round(d['ms_per_step'],4), round(d['pipelined']['ms_per_step'],4), k)")"
   done
 done

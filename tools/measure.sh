@@ -24,4 +24,4 @@ for p in fetch write mfma; do
 done
 python3 tools/pmc_summary.py gpurun_out/pmc_m_$tag --traffic $out/traffic.json > $out/pmc_traffic.txt 2>&1
 python3 tools/mfma_util.py gpurun_out/pmc_m_$tag/mfma --json $out/mfma_util.json > $out/mfma_util.txt 2>&1
-python3 -c "import json;d=json.load(open('$out/bench.json'));print('value', round(d['value']), 'seq', round(d['sequential']['value']), 'roofline', d['roofline']['kernel'], round(d['roofline']['frac'],3))"
+python3 -c "import json;d=json.load(open('$out/bench.json'));print('value', round(d['value']), 'pipe', round(d['pipelined']['value']), 'roofline', d['roofline']['kernel'], round(d['roofline']['frac'],3))"
