@@ -1956,7 +1956,7 @@ __device__ __forceinline__ void screen_bfly16_swap(uint32_t (&k1)[16], uint32_t 
 
 template <int NB>
 __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], int row0, int G0, const float (&bv)[NB],
-                                                   const float2* __restrict__ gs, const float* __restrict__ un_blk,
+                                                   const float2* __restrict__ gsb, const float* __restrict__ un_blk,
                                                    int c0, int V, int B, int NTn, float4* __restrict__ summ) {
   const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
   uint32_t k1[NB][16], k2[NB][16];
@@ -1991,7 +1991,7 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
     if (!(li & 1) && row < B) {
       float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
       if (m1) {
-        const float2 gsv = gs[G0 + b];
+        const float2 gsv = gsb[b];
         const float uw = uw0 * gsv.x;
         const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
         const float x1 = key_value(m1 & ~31u);
@@ -2009,7 +2009,8 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
 template <int H>
 __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8* __restrict__ ua,
                                              const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                             bf16x8 (*Ws)[SC2_STAGE], float* un_s, floatx16 (&acc)[SC2_NB]) {
+                                             bf16x8 (*Ws)[SC2_STAGE], float* un_s, floatx16 (&acc)[SC2_NB],
+                                             const float2* __restrict__ gs = nullptr, float2* gs_s = nullptr) {
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   // this wave's u fragments (row block m0 / 32 + wave) and the W stages arrive AA_SCREEN_AHEAD stages
@@ -2044,17 +2045,20 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
   };
 #pragma unroll
   for (int s = 0; s < AH; ++s) uload(s, s);
-  // epilogue operand, loaded behind the fragments
-  if (t < SC2_BM) {
-    const int r = m0 + t;
-    un_s[t] = unorm[r < B ? r : B - 1];
-  }
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 #pragma unroll
   for (int s = 0; s < AH; ++s) gload(s, s);
+  // epilogue operands, loaded behind the first stages' fragments (storing them to LDS waits for
+  // those stages, which the first MFMAs wait for anyway)
+  if (t < SC2_BM) {
+    const int r = m0 + t;
+    un_s[t] = unorm[r < B ? r : B - 1];
+  } else if (gs_s && t < SC2_BM + SC2_NB) {  // the granule bound factors, staged with ||u||
+    gs_s[t - SC2_BM] = gs[n0 / VS_TILE + t - SC2_BM];
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     lstore(s & 1, s % RW);
@@ -2082,6 +2086,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
                                                   float4* __restrict__ summ) {
   __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
   __shared__ float un_s[SC2_BM];
+  __shared__ float2 gs_s[SC2_NB];
   AA_TS(2, 0);
   const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
   const int L = xcd_remap(blockIdx.x, MT * NT);
@@ -2092,14 +2097,20 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b) bvs[b] = bias[n0 + 32 * b + li];
   floatx16 acc[SC2_NB];
-  screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc);
+#ifndef AA_SCREEN_GS_LDS
+#define AA_SCREEN_GS_LDS 1
+#endif
+  // the granule bounds reach the epilogue through LDS (loaded before the main loop, no registers held
+  // across it) instead of by global loads inside the epilogue
+  screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc, AA_SCREEN_GS_LDS ? gs : nullptr, gs_s);
   AA_TS(2, 1);
   const int row0 = m0 + 32 * wave;
 #ifndef AA_SCREEN_EPI
 #define AA_SCREEN_EPI 1
 #endif
 #if AA_SCREEN_EPI
-  screen_blocks_summ<SC2_NB>(acc, row0, n0 / VS_TILE, bvs, gs, un_s + 32 * wave, n0, V, B, NTn, summ);
+  screen_blocks_summ<SC2_NB>(acc, row0, n0 / VS_TILE, bvs, AA_SCREEN_GS_LDS ? gs_s : gs + n0 / VS_TILE,
+                             un_s + 32 * wave, n0, V, B, NTn, summ);
 #else
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b) {

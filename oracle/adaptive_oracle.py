@@ -194,12 +194,14 @@ class BeamOracle(OracleModel):
 
     @torch.no_grad()
     def beam_search(self, images: torch.Tensor, max_len: int = 20, beam_size: int = 3, end_id: int = 2,
-                    return_margin: bool = False):
+                    return_margin: bool = False, return_steps: bool = False):
         """-> ids [B,T], alpha [B,T,49], beta [B,T,1], seqs [B,K,T], scores [B,K] (+ margin: the
         smallest gap, over images and steps, between consecutive candidates among the K+1 best —
-        how much score error the selection and its order can absorb)."""
+        how much score error the selection and its order can absorb; + with ``return_steps`` a list
+        over steps of (per-image smallest such gap [B], the K surviving cumulative scores [B,K]))."""
         K = beam_size
         margin = float("inf")
+        steps = []
         V, v_g, (h, c), _ = self.encoder(images)
         B = images.size(0)
         Vk = V.repeat_interleave(K, 0)
@@ -224,10 +226,12 @@ class BeamOracle(OracleModel):
             vals, idx = torch.sort(cand.view(B, K * nv), dim=1, descending=True, stable=True)
             top = vals[:, :K + 1]
             gaps = top[:, :-1] - top[:, 1:]
+            per_img = torch.where(torch.isfinite(gaps), gaps, torch.full_like(gaps, float("inf"))).min(1).values
             gaps = gaps[torch.isfinite(gaps)]
             if gaps.numel():
                 margin = min(margin, float(gaps.min()))
             vals, idx = vals[:, :K], idx[:, :K]
+            steps.append((per_img, vals.clone()))
             parent, token = idx // nv, idx % nv
             cum = vals
             fin = fin.gather(1, parent) | ((token == end_id) if end_id >= 0 else torch.zeros_like(fin))
@@ -251,6 +255,5 @@ class BeamOracle(OracleModel):
             be[:, t, 0] = hbe[t][torch.arange(B), p[:, 0]]
             j = p
         ids = seqs[:, 0].clone()
-        if return_margin:
-            return ids, al, be, seqs, cum, margin
-        return ids, al, be, seqs, cum
+        out = (ids, al, be, seqs, cum) + ((margin,) if return_margin else ()) + ((steps,) if return_steps else ())
+        return out
