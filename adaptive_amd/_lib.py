@@ -139,7 +139,10 @@ def load() -> ctypes.CDLL:
                 "`make -C adaptive_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`. "
                 "There is no CPU fallback.")
         lib = ctypes.CDLL(LIB_PATH)
+        partial = bool(os.environ.get("AA_LIB_PATH"))  # A/B builds may be greedy-only (AA_DECODE_ONLY)
         for name, (res, args) in SIGNATURES.items():
+            if partial and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -170,12 +170,21 @@ __global__ __launch_bounds__(256) void k_gsumm(int R, int V, int Vp, const float
 
 // k_vexact (the beam's default vocab stage): exact fp32 logits -- k_vocab's arithmetic (the same
 // v_mfma_f32_32x32x2f32 sequence over NP_VOCAB chains and the same combination tree, via
-// gemm_mainloop_chain), so the same bits -- on 128 x 64 tiles (each wave 64 x 32: two blocks, where
-// k_vocab's 64 x 64 tiles give each wave one block and hold all 8 chains), with the granule summaries
-// of k_gsumm fused into the epilogue (granule_summary on the same values: the same bits).
+// gemm_mainloop_chain: the 8 chains combined as they complete, so a wave holds 4 partial sets instead
+// of k_vocab's 8), so the same bits -- with the granule summaries of k_gsumm fused into the epilogue
+// (granule_summary on the same values: the same bits).
 // k_vocab + k_gsumm stay as the cross-check path (AA_DECODE_EXACT_VOCAB).
-constexpr int VX_BM = 128, VX_BN = 64;
-__global__ __launch_bounds__(256, 1) void k_vexact(int R, int H, int V, int Vp, const float* __restrict__ u,
+// 64 x 64 tiles (3,840 workgroups at config 4, 200 VGPRs: two workgroups per CU) measured 0.187 ms per
+// launch against 0.212 ms for 128 x 64 tiles (1,920 workgroups, 384 registers: one wave per SIMD, the
+// LDS and barrier latencies exposed); beams bitwise unchanged (round 3, A/B on one box)
+#ifndef AA_VX_BM
+#define AA_VX_BM 64
+#endif
+constexpr int VX_BM = AA_VX_BM, VX_BN = 64;
+#ifndef AA_VEXACT_OCC
+#define AA_VEXACT_OCC 1
+#endif
+__global__ __launch_bounds__(256, AA_VEXACT_OCC) void k_vexact(int R, int H, int V, int Vp, const float* __restrict__ u,
                                                    const float* __restrict__ W, const float* __restrict__ bias,
                                                    float* __restrict__ logits, float2* __restrict__ gsum) {
   __shared__ __attribute__((aligned(16))) float lds[Tile<VX_BM, VX_BN>::LDS_FLOATS];

@@ -431,12 +431,19 @@ constexpr int E4_ROWS = 98, E4_RB = 7, E4_LD = 48;  // rows per workgroup, 16-ro
 constexpr int E4_SP = 52, E4_MAXC = 2048;           // a_g staging pitch (floats), largest channel count
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-template <int NCB>
-__global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats, int B, int C,
+// NW waves (8 or 16): each wave owns NCB 16-column blocks (H = 16 NCB NW); the A staging is done by
+// the first 512 threads either way (NW = 16: four waves per SIMD instead of two, half the columns each)
+#ifndef AA_ENC4_NW
+#define AA_ENC4_NW 8
+#endif
+template <int NCB, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ feats, int B, int C,
                                                 const bf16x8* __restrict__ W4, const float* __restrict__ bias,
                                                 float* __restrict__ V, float* __restrict__ a_g) {
   static_assert(NCB % 2 == 0, "columns are processed in pairs of 16-column blocks");
-  constexpr int H = 128 * NCB, NPAIR = NCB / 2, PL = E4_RB * 16 * E4_LD;  // PL: one plane, bf16
+  constexpr int H = 16 * NCB * NW, NPAIR = NCB / 2, PL = E4_RB * 16 * E4_LD;  // PL: one plane, bf16
+  constexpr int NT = 64 * NW;
+  const bool stager = NW == 8 || threadIdx.x < 512;
   __shared__ __attribute__((aligned(16))) __bf16 As[2][3][PL];
   __shared__ __attribute__((aligned(16))) float Sg[2][2 * 32 * E4_SP];  // fp32 stage copy for a_g
   __shared__ __attribute__((aligned(16))) float Ag[2 * E4_MAXC];        // a_g of the two images
@@ -491,17 +498,19 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
   };
 
   const int ns = KC;
-  gload_a(0);
+  if (stager) gload_a(0);
 #pragma unroll
   for (int c = 0; c < NCB; ++c) gload_w(0, c);
-  lstore_a(0);
-  gload_a(ns > 1 ? 1 : 0);
+  if (stager) lstore_a(0);
+  if (stager) gload_a(ns > 1 ? 1 : 0);
   __syncthreads();
   for (int s = 0; s < ns; ++s) {
     const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
     // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
-    lstore_a(buf ^ 1);
-    gload_a(s2);
+    if (stager) {
+      lstore_a(buf ^ 1);
+      gload_a(s2);
+    }
     __builtin_amdgcn_sched_barrier(0);
     const __bf16* Ab = &As[buf][0][fo];
 #pragma unroll
@@ -552,7 +561,7 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
     __builtin_amdgcn_sched_barrier(0);
   }
   // a_g of the workgroup's images (the last workgroup of an odd batch holds one)
-  for (int i = t; i < 2 * C; i += 512) {
+  for (int i = t; i < 2 * C; i += NT) {
     const int img = 2 * blockIdx.x + (i >= C);
     if (img < B) a_g[(int64_t)img * C + (i - (i >= C ? C : 0))] = Ag[i];
   }
@@ -579,7 +588,7 @@ __global__ __launch_bounds__(512) void k_enc_v4(const float* __restrict__ feats,
     __syncthreads();
     constexpr int F4 = 16 * H / 4;  // float4s of the block
 #pragma unroll
-    for (int q = t; q < F4; q += 512) {
+    for (int q = t; q < F4; q += NT) {
       const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
       if (tr < E4_ROWS && row < M)
         *reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4) = *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4);
@@ -1595,10 +1604,23 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   }
   const float* vb = Vf + (int64_t)img * P * H;
   float vv[DPT][P];
+  // AA_ATTEN_VA: V rows issued before the small operands above are waited for; the rest of V is issued
+  // once they have landed, so the score chain's loads do not queue behind the whole V stream
+#ifndef AA_ATTEN_VA
+#define AA_ATTEN_VA P
+#endif
+  constexpr int VA = AA_ATTEN_VA < P ? AA_ATTEN_VA : P;
 #pragma unroll
   for (int i = 0; i < DPT; ++i)
 #pragma unroll
-    for (int kk = 0; kk < P; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
+    for (int kk = 0; kk < VA; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
+  if constexpr (VA < P) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VA * DPT) : "memory");
+#pragma unroll
+    for (int i = 0; i < DPT; ++i)
+#pragma unroll
+      for (int kk = VA; kk < P; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
+  }
   float hv[DPT], sv[DPT];
 #pragma unroll
   for (int i = 0; i < DPT; ++i) {
@@ -2121,6 +2143,127 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
   AA_TS(2, 2);
 }
 
+// Screen, LDS-DMA form (k_vscreen4, AA_SCREEN_DMA=1 builds; measured slower, so not the default):
+// k_vscreen2's tile, waves, MFMA order and
+// epilogue (bit-identical summaries), but every operand reaches LDS by LDS-DMA (global_load_lds, 1 KB
+// per wave instruction) into an SC4_NB-slot ring, with no register staging, no ds_write and no
+// ordinary global load in flight beside the DMAs (hipcc would drain the DMAs before the first use of
+// one).  A stage = SC2_KS k16 chunks of the tile's 4 u row blocks and 5 W column blocks = 36 fragments
+// (36 KB), 9 issued by each wave; SC4_NB - 1 stages stay in flight while one is multiplied.  The
+// epilogue's operands (||u|| of the 128 rows, the 160 biases, the 5 granule bound factors) arrive by
+// one more DMA per wave before the ring, so the whole kernel has no exposed round trip but the ring's.
+// Measured (round 3, A/B of two builds on one box, two rounds, HIP events): k_vscreen2 14.4 / 14.2 us,
+// k_vscreen4 15.5 / 16.0 us (3-slot ring 15.9 / 15.8); parity green (bit-identical summaries).  The
+// 36 LDS-DMA wave instructions per stage cost more issue time than the register staging they replace:
+// the screen's main loop is not bound by its bytes in flight.
+#ifndef AA_SCREEN_DMA
+#define AA_SCREEN_DMA 0
+#endif
+#ifndef AA_SC4_NB
+#define AA_SC4_NB 4
+#endif
+constexpr int SC4_NB = AA_SC4_NB, SC4_FPW = (4 + SC2_NB) * SC2_KS / 4;  // ring slots; fragments per wave per stage
+constexpr int SC4_STAGE = 4 * SC4_FPW * 64;                             // bf16x8 per stage
+static_assert(SC4_FPW * 4 == (4 + SC2_NB) * SC2_KS, "a stage's fragments split evenly over the 4 waves");
+
+template <int H>
+__global__ __launch_bounds__(256, 1) void k_vscreen4(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                  float4* __restrict__ summ) {
+  constexpr int KC = H / 16, NS = KC / SC2_KS, NB = SC4_NB < NS ? SC4_NB : NS;
+  static_assert(NB >= 2, "the ring needs two slots");
+  __shared__ __attribute__((aligned(16))) bf16x8 ring[NB * SC4_STAGE];
+  __shared__ __attribute__((aligned(16))) float ep[SC2_BM + 4 * 64 + 64];  // ||u|| [128], bias [256], gs [64]
+  AA_TS(2, 0);
+  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NT);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  // epilogue operands, one DMA per wave (lanes past the end re-read the last valid element)
+  typedef __attribute__((address_space(3))) void lds_t;
+  if (wave < 2) {  // ||u|| of rows m0 + 64 wave + lane
+    const int r = m0 + 64 * wave + lane;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(unorm + (r < B ? r : B - 1)),
+                                     (lds_t*)(ep + 64 * wave), 4, 0, 0);
+  } else if (wave == 2) {  // the 160 biases as 40 float4
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(bias + n0 + 4 * (lane < 40 ? lane : 39)),
+                                     (lds_t*)(ep + SC2_BM), 16, 0, 0);
+  } else {  // the 5 granules' (max ||w||, max |b|) as 10 floats
+    const float* g = reinterpret_cast<const float*>(gs + n0 / VS_TILE);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + (lane < 2 * SC2_NB ? lane : 2 * SC2_NB - 1)),
+                                     (lds_t*)(ep + SC2_BM + 256), 4, 0, 0);
+  }
+  // fragment f of a stage: f < 16 -> u row block f / 4, chunk f % 4; else W column block (f - 16) / 4,
+  // chunk (f - 16) % 4; wave w issues f = 9 w .. 9 w + 8; stage s adds 4 s chunks
+  const bf16x8* src[SC4_FPW];
+#pragma unroll
+  for (int i = 0; i < SC4_FPW; ++i) {
+    const int f = SC4_FPW * wave + i;
+    src[i] = f < 16 ? ua + ((size_t)((m0 >> 5) + f / 4) * KC + f % 4) * 64 + lane
+                    : wf + ((size_t)((n0 >> 5) + (f - 16) / 4) * KC + (f - 16) % 4) * 64 + lane;
+  }
+  auto issue = [&](int s) {
+    bf16x8* dst = ring + (s % NB) * SC4_STAGE + SC4_FPW * wave * 64;
+#pragma unroll
+    for (int i = 0; i < SC4_FPW; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)s * SC2_KS * 64),
+                                       (lds_t*)(dst + i * 64), 16, 0, 0);
+  };
+  // chunk c of stage s into register set: this wave's u fragment and the 5 W fragments
+  bf16x8 fa[2], fw[2][SC2_NB];
+  auto lread = [&](int s, int c, int set) {
+    const bf16x8* sb = ring + (s % NB) * SC4_STAGE + lane;
+    fa[set] = sb[(4 * wave + c) * 64];
+#pragma unroll
+    for (int b = 0; b < SC2_NB; ++b) fw[set][b] = sb[(16 + 4 * b + c) * 64];
+  };
+  floatx16 acc[SC2_NB];
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < NB; ++s) issue(s);
+  __builtin_amdgcn_sched_barrier(0);
+  // stage 0 landed (younger: stages 1 .. NB-1); the epilogue DMA is older
+  vm_wait(SC4_FPW * (NB - 1));
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  lread(0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int c = 0; c < SC2_KS; ++c) {
+      const int set = c & 1;
+      if (c + 1 < SC2_KS) {
+        lread(s, c + 1, set ^ 1);
+      } else if (s + 1 < NS) {
+        // stage s + 1 landed: younger are the stages issued after it (up to s + NB - 1)
+        const int last = s + NB - 1 < NS - 1 ? s + NB - 1 : NS - 1;
+        vm_wait(SC4_FPW * (last - (s + 1)));
+        // every wave's reads of stage s retired before its slot is refilled
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (s + NB < NS) issue(s + NB);
+        lread(s + 1, 0, set ^ 1);
+      }
+#pragma unroll
+      for (int b = 0; b < SC2_NB; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set], fw[set][b], acc[b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  AA_TS(2, 1);
+  float bvs[SC2_NB];
+#pragma unroll
+  for (int b = 0; b < SC2_NB; ++b) bvs[b] = ep[SC2_BM + 32 * b + (lane & 31)];
+  screen_blocks_summ<SC2_NB>(acc, m0 + 32 * wave, n0 / VS_TILE, bvs,
+                             reinterpret_cast<const float2*>(ep + SC2_BM + 256), ep + 32 * wave, n0, V, B, NTn, summ);
+  AA_TS(2, 2);
+}
+
 // Exact fp32 logit of one column, computed by a group of 8 lanes (lane8 = 0..7): lane8 j runs the
 // fma chain of partial j (K-steps [j*per, (j+1)*per) of 32, in the MFMA k order: pairs (s, 16+s)),
 // then the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) over xor-1/2/4 shuffles, then + bias.
@@ -2522,11 +2665,12 @@ __global__ __launch_bounds__(256) void k_vocab(int B, int H, int V, int Vp, int 
   }
 }
 
-__global__ void k_finalize(const uint64_t* __restrict__ keys, int B, int T, int64_t* __restrict__ ids) {
+// ids [B][T] from the argmax keys [T][ldk] (ldk = the whole batch when B is a lane's row block)
+__global__ void k_finalize(const uint64_t* __restrict__ keys, int B, int T, int64_t* __restrict__ ids, int ldk) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * T) return;
   const int b = (int)(i / T), t = (int)(i % T);
-  ids[i] = key_token(keys[(int64_t)t * B + b]);
+  ids[i] = key_token(keys[(int64_t)t * ldk + b]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2761,6 +2905,10 @@ static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
 // Encoder tail.  With an aux stream, the a_g branch (k_avgpool -> k_enc_heads -> x_g GEMM: HBM- and
 // latency-bound) runs beside the V branch (k_enc_v3 -> VWv GEMM: MFMA-bound); both read only the
 // features, and `s` waits for aux before returning.
+// the encoder's V GEMM runs on k_enc_v4 (which also writes the compressed V when asked)
+static bool enc_v4(const Layout& L, int32_t flags) {
+  return !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && (L.H == 512 || L.H == 256) && L.C <= E4_MAXC;
+}
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
                           hipStream_t s, hipStream_t aux = nullptr) {
@@ -2794,7 +2942,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
     rec(ev, 9, st);
   };
-  const bool v4 = !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && (H == 512 || H == 256) && C <= E4_MAXC;
+  const bool v4 = enc_v4(L, flags);
   if (v4) {
     // k_enc_v4 computes V and a_g in one pass over the feature map; the a_g branch (heads, x_g)
     // then runs on aux beside the VWv GEMM.  (Trace: the fused avg-pool is a zero-length pair.)
@@ -2803,7 +2951,8 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     rec(ev, 2, s);
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
     if (H == 512)
-      hipLaunchKernelGGL(k_enc_v4<4>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+      hipLaunchKernelGGL((k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg),
+                         dim3(64 * AA_ENC4_NW), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
     else
       hipLaunchKernelGGL(k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
     rec(ev, 3, s);
@@ -2954,8 +3103,8 @@ static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok,
 #define AA_LSTM(H_)                                                                                          \
   do {                                                                                                       \
     if (par)                                                                                                 \
-      hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, \
-                         xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);           \
+      hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
+                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part); \
     else                                                                                                     \
       hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
                          p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);  \
@@ -3075,7 +3224,7 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
                     nullptr, nullptr, alpha, P, beta, 1, nullptr, 0, s);
   hipLaunchKernelGGL(k_vocab, dim3(((B + 63) / 64) * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V, w.u, p.mlp_w,
                      p.mlp_b, scores, w.keys);
-  hipLaunchKernelGGL(k_finalize, dim3((B + 255) / 256), dim3(256), 0, s, w.keys, B, 1, tokens_out);
+  hipLaunchKernelGGL(k_finalize, dim3((B + 255) / 256), dim3(256), 0, s, w.keys, B, 1, tokens_out, B);
   return launch_status();
 }
 
@@ -3176,7 +3325,8 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
       rec(aev, 2 * t + 1, s);
     } else {
       lstm_atten_launch(L, p, Bl, tok, tok_ld, V, vwv, xg, hs[cur], cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, u,
-                        exact ? nullptr : ub, exact ? nullptr : unorm, alt, (int64_t)T * P, blt, T, trace, t, s);
+                        exact ? nullptr : ub, exact ? nullptr : unorm, alt, (int64_t)T * P, blt, T, trace, t, s,
+                        nullptr, 1, nullptr);
     }
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
@@ -3192,7 +3342,8 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
                      L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                        \
                      reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
 #define AA_SCREEN2(H_)                                                                                      \
-  hipLaunchKernelGGL(k_vscreen2<H_>, dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl, \
+  hipLaunchKernelGGL((AA_SCREEN_DMA && H_ == 512 ? k_vscreen4<H_> : k_vscreen2<H_>),                          \
+                     dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl,                 \
                      L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
                      reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
 #define AA_SCREEN3(H_)                                                                                      \
@@ -3465,7 +3616,11 @@ int aa_synth_uniform(float* dst, int64_t n, uint64_t key, int64_t start, double 
   return launch_status();
 }
 
+// AA_DECODE_ONLY: A/B variant builds of the greedy path only (tools/build_variant.sh; the training
+// and beam entry points are then absent and adaptive_amd._lib binds only what the library exports)
+#ifndef AA_DECODE_ONLY
 // teacher-forced training step (same translation unit: reuses the encoder kernels)
 #include "aa_train.hip"
 // beam-search decode (reuses k_lstm / k_atten / k_vocab and the encoder)
 #include "aa_beam.hip"
+#endif

@@ -243,13 +243,29 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   }
 }
 
+// value i of a split GEMM: its S partials summed in split order from 0 (+ 0, as the reduce adds absent
+// biases), or src itself when it was not split.  Up to SK_MAX partials are loaded together before the
+// ordered sum (a loop over a runtime count waits for each load in turn).
+constexpr int SK_MAX = 16;
+__device__ __forceinline__ float sk_sum(const float* __restrict__ src, int S, int64_t MN, int64_t i) {
+  if (S == 1) return src[i];
+  float x[SK_MAX];
+#pragma unroll
+  for (int sp = 0; sp < SK_MAX; ++sp) x[sp] = sp < S ? src[sp * MN + i] : 0.f;
+  float v = 0.f;
+#pragma unroll
+  for (int sp = 0; sp < SK_MAX; ++sp)
+    if (sp < S) v += x[sp];
+  for (int sp = SK_MAX; sp < S; ++sp) v += src[sp * MN + i];
+  return v + 0.f;
+}
+
 // split-K epilogue: partials summed in split order, then bias / act / row map / accumulate
 __global__ void k_tgemm_reduce(TG g) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)g.M * g.N) return;
   const int m = (int)(i / g.N), n = (int)(i % g.N);
-  float v = 0.f;
-  for (int sp = 0; sp < g.splits; ++sp) v += g.part[(int64_t)sp * g.M * g.N + i];
+  float v = sk_sum(g.part, g.splits, (int64_t)g.M * g.N, i);
   v += (g.bias ? g.bias[n] : 0.f) + (g.bias2 ? g.bias2[n] : 0.f);
   if (g.act == 1) v = reluf_(v);
   else if (g.act == 2) v = tanhf(v);
@@ -267,10 +283,15 @@ struct GemmCtx {
 
 // C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites.  GEMMs with
 // too few output tiles to fill the chip are split along K (deterministically reduced).
-static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t lda, int at, const float* W, int64_t ldw,
-                  int wm, float* C, int64_t ldc, int accumulate = 0, const float* bias = nullptr,
-                  const float* bias2 = nullptr, int act = 0, const int* arow = nullptr, const int* crow = nullptr) {
-  if (M <= 0 || N <= 0) return;
+// `defer` (the recurrent LSTM GEMMs): a split-K GEMM leaves its partial tiles in gc.split and
+// returns the split count, and the consumer (k_tr_cell_sk / k_tr_cell_bwd_sk) sums them in split order
+// itself -- k_tgemm_reduce's arithmetic, one launch fewer per recurrent step; 1 = C written (no split,
+// no bias / act / accumulate allowed with defer).
+static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t lda, int at, const float* W, int64_t ldw,
+                 int wm, float* C, int64_t ldc, int accumulate = 0, const float* bias = nullptr,
+                 const float* bias2 = nullptr, int act = 0, const int* arow = nullptr, const int* crow = nullptr,
+                 bool defer = false) {
+  if (M <= 0 || N <= 0) return 0;
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
   int splits = 1;
   const hipStream_t s = gc.s;
@@ -297,9 +318,11 @@ static void tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_
     hipLaunchKernelGGL(k_tgemm<true>, dim3(tiles * splits), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(k_tgemm<false>, dim3(tiles * splits), dim3(256), 0, s, g);
-  if (splits > 1)
+  if (splits > 1 && !defer)
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
+  return splits;
 }
+
 
 // column sums: out[n] (+)= sum_m X[m ldx + n], deterministic: rows split into CS_CH fixed chunks
 // summed in order by k_colsum (one thread per (column, chunk)), the chunk sums added in chunk
@@ -340,17 +363,19 @@ __global__ void k_tr_x(const int64_t* __restrict__ tok, int tld, const float* __
   }
 }
 
-// LSTM cell of step t (torch gate order i, f, g, o): gates = G4 (h W_hh^T) + PRE (x W_ih^T + b)
-__global__ void k_tr_cell(const float* __restrict__ G4, const float* __restrict__ PRE, int ldp,
-                          const float* __restrict__ c_prev, int B, int H, float* __restrict__ h_out,
-                          float* __restrict__ c_out, float* __restrict__ GA) {
+// LSTM cell of step t (torch gate order i, f, g, o): gates = G4 (h W_hh^T) + PRE (x W_ih^T + b), with
+// the recurrent GEMM's split-K reduction folded in: G4 (b, n) = sk_sum(src, S, B 4H, .) (bit-identical
+// to k_tgemm_reduce followed by a plain cell kernel; one launch per step fewer)
+__global__ void k_tr_cell_sk(const float* __restrict__ src, int S, const float* __restrict__ PRE, int ldp,
+                             const float* __restrict__ c_prev, int B, int H, float* __restrict__ h_out,
+                             float* __restrict__ c_out, float* __restrict__ GA) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * H) return;
   const int b = (int)(i / H), j = (int)(i % H);
-  const float* g = G4 + (int64_t)b * 4 * H;
+  const int64_t MN = (int64_t)B * 4 * H, g0 = (int64_t)b * 4 * H + j;
   const float* p = PRE + (int64_t)b * ldp;
-  const float gi = g[j] + p[j], gf = g[H + j] + p[H + j], gg = g[2 * H + j] + p[2 * H + j],
-              go = g[3 * H + j] + p[3 * H + j];
+  const float gi = sk_sum(src, S, MN, g0) + p[j], gf = sk_sum(src, S, MN, g0 + H) + p[H + j],
+              gg = sk_sum(src, S, MN, g0 + 2 * H) + p[2 * H + j], go = sk_sum(src, S, MN, g0 + 3 * H) + p[3 * H + j];
   const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
   const float c = f_ * c_prev[i] + i_ * g_;
   c_out[i] = c;
@@ -613,18 +638,21 @@ __global__ void k_tr_sent_bwd(const float* __restrict__ dS, const float* __restr
   dC[i] = ds * sg * (1.f - tc * tc);
 }
 
-// LSTM cell backward of step t (rows b < B): dh = dH[t] + dh_rec, dc = dC[t] + dc_rec;
-// writes DG[t] (pre-activation gate grads) and dc_rec <- dc * f
-__global__ void k_tr_cell_bwd(const float* __restrict__ dH, const float* __restrict__ dC, const float* __restrict__ dh_rec,
-                              float* __restrict__ dc_rec, const float* __restrict__ GA, const float* __restrict__ c_t,
-                              const float* __restrict__ c_prev, int B, int H, float* __restrict__ DG) {
+// LSTM cell backward of step t (rows b < B): dh = dH[t] + dh_rec, dc = dC[t] + dc_rec; writes DG[t]
+// (pre-activation gate grads) and dc_rec <- dc * f.  The later step's recurrent GEMM dh_rec =
+// DG_{t+1} W_hh is folded in: dh_rec (b, j) = sk_sum(src, S, B H, .), S = 0 at the last step
+// (dh_rec = 0) -- bit-identical to k_tgemm_reduce followed by a plain cell-backward kernel
+__global__ void k_tr_cell_bwd_sk(const float* __restrict__ dH, const float* __restrict__ dC, const float* __restrict__ src,
+                                 int S, float* __restrict__ dc_rec, const float* __restrict__ GA,
+                                 const float* __restrict__ c_t, const float* __restrict__ c_prev, int B, int H,
+                                 float* __restrict__ DG) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * H) return;
   const int b = (int)(i / H), j = (int)(i % H);
   const float* ga = GA + (int64_t)b * 4 * H;
   const float i_ = ga[j], f_ = ga[H + j], g_ = ga[2 * H + j], o_ = ga[3 * H + j];
   const float c = c_t[i], tc = tanhf(c);
-  const float dh = dH[i] + dh_rec[i];
+  const float dh = dH[i] + (S > 0 ? sk_sum(src, S, (int64_t)B * H, i) : 0.f);
   float dc = dC[i] + dc_rec[i] + dh * o_ * (1.f - tc * tc);
   const float d_o = dh * tc;
   const float d_i = dc * g_, d_g = dc * i_, d_f = dc * c_prev[i];
@@ -857,10 +885,11 @@ static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const Train
   for (int t = 0; t < T; ++t) {
     const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
     const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
-    tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H);
-    hipLaunchKernelGGL(k_tr_cell, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.G4, s.PRE + (size_t)t * B * 5 * H,
-                       5 * H, cp, B, H, s.Hs + (size_t)t * B * H, s.Cs + (size_t)t * B * H,
-                       s.GA + (size_t)t * B * 4 * H);
+    const int S = tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H, 0, nullptr, nullptr, 0, nullptr,
+                        nullptr, true);
+    hipLaunchKernelGGL(k_tr_cell_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, S > 1 ? gc.split : s.G4, S,
+                       s.PRE + (size_t)t * B * 5 * H, 5 * H, cp, B, H, s.Hs + (size_t)t * B * H,
+                       s.Cs + (size_t)t * B * H, s.GA + (size_t)t * B * 4 * H);
   }
   // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
   hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
@@ -1038,12 +1067,16 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   // LSTM backward through time (baseline_attention.py:167-178)
   AA_TRY(hipMemsetAsync(s.dh_rec, 0, sizeof(float) * (size_t)B * H, st));
   AA_TRY(hipMemsetAsync(s.dc_rec, 0, sizeof(float) * (size_t)B * H, st));
+  int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
   for (int t = T - 1; t >= 0; --t) {
     const size_t o = (size_t)t * B * H;
     const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
-    hipLaunchKernelGGL(k_tr_cell_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o, s.dh_rec,
-                       s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H, s.DG + (size_t)t * B * 4 * H);
-    tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);  // dh_{t-1}
+    hipLaunchKernelGGL(k_tr_cell_bwd_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o,
+                       S > 1 ? gc.split : s.dh_rec, S, s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H,
+                       s.DG + (size_t)t * B * 4 * H);
+    // dh_{t-1}; the one of step 0 (into h0) is reduced into dh_rec itself
+    S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H, 0, nullptr,
+              nullptr, 0, nullptr, nullptr, t > 0);
   }
   tgemm(gc, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
   tgemm(gc, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);

@@ -6,8 +6,9 @@ set -eu
 name=$1; rev=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/tools/_build"
-if [ "$rev" = WORK ]; then
-  src=$ROOT
+if [ "$rev" = WORK ]; then  # a snapshot: hipcc reads the sources again for its host pass
+  src=$(mktemp -d /tmp/aa_variant.XXXXXX)
+  mkdir -p "$src/adaptive_amd" && cp -r "$ROOT/adaptive_amd/csrc" "$src/adaptive_amd/" && cp -r "$ROOT/include" "$src/"
 else
   src=$(mktemp -d /tmp/aa_variant.XXXXXX)
   git -C "$ROOT" archive "$rev" adaptive_amd/csrc include | tar -x -C "$src"
