@@ -65,7 +65,7 @@ struct Layout {
   int NH, NHp;   // heads rows E + 2H, padded to 64
   int Vp;        // vocab rows padded to 128
   int N5;        // 5H: 4 gates (packed tile order) + sentinel
-  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3, enc_w4, heads_w4;
+  size_t enc_a_w, enc_a_b, enc_w3, whh3, heads_w, heads_b, wv, wg, ws, wh, whh, wemb, wvg, bias5, table, mlp_w, mlp_b, mlp_wb, mlp_wn, mlp_gs, wgs, mlp_w3, enc_w4, heads_w4, wvg4, wv4;
   size_t total_floats;
 };
 
@@ -104,12 +104,14 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_w3 = take((size_t)3 * L.Vp * L.H / 2);    // W_m as 3 bf16 planes, fragments [Vp/32][H/16][3][64][8] (beam)
   L.enc_w4 = take((size_t)3 * L.H * L.C / 2);     // W_a as 3 bf16 planes, 16x16x32 fragments [H/16][C/32][3][64][8]
   L.heads_w4 = take((size_t)3 * L.NHp * L.C / 2);  // heads as 3 bf16 planes, 16x16x32 fragments [NHp/16][C/32][3][64][8]
+  L.wvg4 = take((size_t)3 * L.N5 * L.E / 2);       // W_vg (x_g GEMM) likewise [N5/16][E/32][3][64][8]
+  L.wv4 = take((size_t)3 * PP * L.H / 2);          // W_v (VWv GEMM) likewise [PP/16][H/32][3][64][8]
   L.total_floats = o;
   return L;
 }
 
 struct MP {  // resolved device pointers of the packed weights
-  const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4, *heads_w4;
+  const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4, *heads_w4, *wvg4, *wv4;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
   const float2* mlp_gs;
@@ -125,6 +127,8 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.mlp_w3 = reinterpret_cast<const bf16x8*>(b + L.mlp_w3);
   p.enc_w4 = reinterpret_cast<const bf16x8*>(b + L.enc_w4);
   p.heads_w4 = reinterpret_cast<const bf16x8*>(b + L.heads_w4);
+  p.wvg4 = reinterpret_cast<const bf16x8*>(b + L.wvg4);
+  p.wv4 = reinterpret_cast<const bf16x8*>(b + L.wv4);
   p.heads_w = b + L.heads_w; p.heads_b = b + L.heads_b;
   p.wv = b + L.wv; p.wg = b + L.wg; p.ws = b + L.ws; p.wh = b + L.wh;
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
@@ -432,9 +436,10 @@ constexpr int E4_SP = 52, E4_MAXC = 2048;           // a_g staging pitch (floats
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // NW waves (8 or 16): each wave owns NCB 16-column blocks (H = 16 NCB NW); the A staging is done by
-// the first 512 threads either way (NW = 16: four waves per SIMD instead of two, half the columns each)
+// the first 512 threads either way.  NW = 16 (four waves per SIMD instead of two, half the columns
+// each; the default at H = 512): k_enc_v4 247 -> 242 us, sequential decode +0.9 % (A/B, two rounds)
 #ifndef AA_ENC4_NW
-#define AA_ENC4_NW 8
+#define AA_ENC4_NW 16
 #endif
 template <int NCB, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ feats, int B, int C,
@@ -546,7 +551,9 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
       // re-read the A fragments for the next pair instead of keeping all 21 live (VGPR budget)
       asm volatile("" ::: "memory");
     }
-    if (wave == (s & 7)) {  // a_g of stage s's 32 channels: lane -> (image lane / 32, channel lane % 32)
+    // one wave per stage (rotating over waves 0..7) sums the stage's channels for a_g (giving the turns
+    // to waves 8..15, which do no A staging, measured 4 us slower at NW = 16)
+    if (wave == (s & 7)) {  // lane -> (image lane / 32, channel lane % 32)
       const float* g = &Sg[buf][lane * E4_SP];
       float sum = 0.f;
 #pragma unroll 4
@@ -627,21 +634,25 @@ __global__ __launch_bounds__(256) void k_enc_heads(const float* __restrict__ a_g
 }
 
 // ---------------------------------------------------------------------------------------------
-// E2 (default): the heads on bf16 MFMA with 3-way split operands (fp32-accurate, as k_enc_v4).
-// k_enc_heads' 64 x 64 fp32-MFMA tiles give 160 workgroups that each run all K = 2048 (≈66 µs);
-// here a workgroup owns 32 rows x 16 NB columns (grid (B/32) x (NHp / 16 NB): 256 workgroups at
-// B = 512, NB = 5), its four waves each run a quarter of K over the whole tile (v_mfma_f32_16x16x32
-// _bf16; a_g fragments split in registers, W pre-split in 16x16x32 B-fragment order, heads_w4), and
-// the four partial tiles are summed in LDS as ((p0 + p1) + (p2 + p3)) before bias and activation.
+// E2 (default): the encoder's small GEMMs on bf16 MFMA with 3-way split operands (fp32-accurate, as
+// k_enc_v4): out[M x N] = A[M x K] W^T (+ bias), A fp32 row-major (lda K), W pre-split in 16x16x32
+// B-fragment order (k_pack_w4).  A workgroup owns 32 rows x 16 NB columns; its NWV waves each run
+// 1/NWV of K over the whole tile (v_mfma_f32_16x16x32_bf16, a fragments split in registers), and the
+// NWV partial tiles are summed in LDS as a fixed pairwise tree before bias and epilogue.  These GEMMs
+// are short (K = 256..2048, 32-row tiles): their time is the K loop's load latency, so K is spread
+// over waves (k_enc_heads' 64 x 64 fp32-MFMA tiles ran all K = 2048 per workgroup: ≈66 µs).
+//   MODE_HEADS: columns [0, E) -> v_g = relu, [E, E+H) -> h0 = tanh, [E+H, E+2H) -> c0 = tanh
+//   MODE_PLAIN: out0[row * ldo + col] = acc + (bias ? bias[col] : 0), col < N  (x_g, VWv)
 // ---------------------------------------------------------------------------------------------
-template <int NB>
-__global__ __launch_bounds__(256) void k_enc_heads3(const float* __restrict__ a_g, int B, int C, int E, int H,
+enum { MODE_HEADS = 0, MODE_PLAIN = 1 };
+template <int NB, int NWV, int MODE>
+__global__ __launch_bounds__(64 * NWV) void k_gemm3(const float* __restrict__ A, int M, int K, int N,
                                                     const bf16x8* __restrict__ W4, const float* __restrict__ bias,
-                                                    float* __restrict__ v_g, float* __restrict__ h0,
-                                                    float* __restrict__ c0) {
+                                                    float* __restrict__ out0, int ldo, float* __restrict__ h0,
+                                                    float* __restrict__ c0, int E, int H) {
   constexpr int BN = 16 * NB, TP = BN + 4;  // tile columns, LDS row pitch of a partial tile (floats)
-  __shared__ __attribute__((aligned(16))) float Pt[4][32 * TP];
-  const int KC = C / 32, NTn = (E + 2 * H + BN - 1) / BN;
+  __shared__ __attribute__((aligned(16))) float Pt[NWV][32 * TP];
+  const int KC = K / 32, NTn = (N + BN - 1) / BN;
   const int mt = blockIdx.x / NTn, nt = blockIdx.x % NTn;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m0 = mt * 32;
@@ -649,8 +660,8 @@ __global__ __launch_bounds__(256) void k_enc_heads3(const float* __restrict__ a_
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
     int m = m0 + 16 * rb + (lane & 15);
-    m = m < B ? m : B - 1;  // clamp, never zero (rows >= B are not stored)
-    arow[rb] = a_g + (int64_t)m * C + 8 * (lane >> 4);
+    m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
+    arow[rb] = A + (int64_t)m * K + 8 * (lane >> 4);
   }
   const bf16x8* wsrc = W4 + (size_t)(nt * NB) * KC * 3 * 64 + lane;
   floatx4 acc[2][NB];
@@ -658,7 +669,7 @@ __global__ __launch_bounds__(256) void k_enc_heads3(const float* __restrict__ a_
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int c = 0; c < NB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int per = KC / 4, kc0 = wave * per;  // C % 256 == 0 (checked by the host): per is even
+  const int per = KC / NWV, kc0 = wave * per;  // K % (64 NWV) == 0 (checked by the host): per is even
   float4 av[2][2][2];   // [slot][row block][half]
   bf16x8 wv[2][NB][3];  // [slot][column block][plane]
   auto load = [&](int slot, int kc) {
@@ -713,14 +724,25 @@ __global__ __launch_bounds__(256) void k_enc_heads3(const float* __restrict__ a_
 #pragma unroll
       for (int i = 0; i < 4; ++i) Pt[wave][(16 * rb + 4 * (lane >> 4) + i) * TP + 16 * c + (lane & 15)] = acc[rb][c][i];
   __syncthreads();
-  for (int e = t; e < 32 * BN; e += 256) {
+  for (int e = t; e < 32 * BN; e += 64 * NWV) {
     const int r = e / BN, cl = e - r * BN, row = m0 + r, col = nt * BN + cl;
-    if (row >= B || col >= E + 2 * H) continue;
+    if (row >= M || col >= N) continue;
     const int o = r * TP + cl;
-    const float x = ((Pt[0][o] + Pt[1][o]) + (Pt[2][o] + Pt[3][o])) + bias[col];
-    if (col < E) v_g[(int64_t)row * E + col] = reluf_(x);
-    else if (col < E + H) h0[(int64_t)row * H + (col - E)] = tanhf(x);
-    else c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
+    float ps[NWV];
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) ps[w] = Pt[w][o];
+#pragma unroll
+    for (int st = 1; st < NWV; st *= 2)  // ((p0 + p1) + (p2 + p3)) + ...
+#pragma unroll
+      for (int w = 0; w + st < NWV; w += 2 * st) ps[w] += ps[w + st];
+    if (MODE == MODE_PLAIN) {
+      out0[(int64_t)row * ldo + col] = bias ? ps[0] + bias[col] : ps[0];
+    } else {
+      const float x = ps[0] + bias[col];
+      if (col < E) out0[(int64_t)row * E + col] = reluf_(x);
+      else if (col < E + H) h0[(int64_t)row * H + (col - E)] = tanhf(x);
+      else c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
+    }
   }
 }
 
@@ -2895,6 +2917,12 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                      reinterpret_cast<bf16x8*>(base + L.enc_w4));
   hipLaunchKernelGGL(k_pack_w4, dim3((L.NHp / 16) * (C / 32)), dim3(64), 0, s, base + L.heads_w, C,
                      reinterpret_cast<bf16x8*>(base + L.heads_w4));
+  if (E % 32 == 0)
+    hipLaunchKernelGGL(k_pack_w4, dim3((L.N5 / 16) * (E / 32)), dim3(64), 0, s, base + L.wvg, E,
+                       reinterpret_cast<bf16x8*>(base + L.wvg4));
+  if (H % 32 == 0)
+    hipLaunchKernelGGL(k_pack_w4, dim3((PP / 16) * (H / 32)), dim3(64), 0, s, base + L.wv, H,
+                       reinterpret_cast<bf16x8*>(base + L.wv4));
   return launch_status();
 }
 
@@ -2908,6 +2936,10 @@ static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
 // the encoder's V GEMM runs on k_enc_v4 (which also writes the compressed V when asked)
 static bool enc_v4(const Layout& L, int32_t flags) {
   return !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && (L.H == 512 || L.H == 256) && L.C <= E4_MAXC;
+}
+// x_g and VWv on k_gemm3 (bf16x3) unless an fp32-MFMA encoder was asked for; K % 256 == 0 (4 waves)
+static bool gemm3_ok(int32_t flags, int K) {
+  return !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && K % 256 == 0;
 }
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
@@ -2930,16 +2962,20 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
       const int MT = (B + 63) / 64, NTn = L.NHp / 64;
       hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
                          v_g, h0, c0);
-    } else if (NH % 80 == 0) {
-      hipLaunchKernelGGL(k_enc_heads3<5>, dim3(((B + 31) / 32) * (NH / 80)), dim3(256), 0, st, a_g, B, C, E, H,
-                         p.heads_w4, p.heads_b, v_g, h0, c0);
+    } else if (NH % 80 == 0 && C % 512 == 0) {
+      hipLaunchKernelGGL((k_gemm3<5, 8, MODE_HEADS>), dim3(((B + 31) / 32) * (NH / 80)), dim3(512), 0, st, a_g, B, C,
+                         NH, p.heads_w4, p.heads_b, v_g, 0, h0, c0, E, H);
     } else {
-      hipLaunchKernelGGL(k_enc_heads3<4>, dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st, a_g, B, C, E,
-                         H, p.heads_w4, p.heads_b, v_g, h0, c0);
+      hipLaunchKernelGGL((k_gemm3<4, 4, MODE_HEADS>), dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st, a_g,
+                         B, C, NH, p.heads_w4, p.heads_b, v_g, 0, h0, c0, E, H);
     }
     rec(ev, 5, st);
     rec(ev, 8, st);
-    if (xg) gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
+    if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0)
+      hipLaunchKernelGGL((k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st, v_g, B, E,
+                         L.N5, p.wvg4, p.bias5, xg, L.N5, nullptr, nullptr, 0, 0);
+    else if (xg)
+      gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
     rec(ev, 9, st);
   };
   const bool v4 = enc_v4(L, flags);
@@ -2980,7 +3016,11 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     rec(ev, 3, s);
   }
   rec(ev, 6, s);
-  if (VWv) gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
+  if (VWv && gemm3_ok(flags, H))
+    hipLaunchKernelGGL((k_gemm3<4, 4, MODE_PLAIN>), dim3((B * P + 31) / 32), dim3(256), 0, s, V, B * P, H, PP, p.wv4,
+                       nullptr, VWv, PP, nullptr, nullptr, 0, 0);
+  else if (VWv)
+    gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
   rec(ev, 7, s);
   if (join) {
     AA_TRY(hipEventRecord(join, sa));
@@ -3412,6 +3452,11 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
+  // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
+  int nl = n_lanes > 0 ? n_lanes : 1;
+  const int tiles = (B + 63) / 64;
+  if (nl > tiles) nl = tiles;
+  if (nl > AA_MAX_LANES) nl = AA_MAX_LANES;
   if (!aux && n_lanes > 1) aux = (hipStream_t)lanes[1];
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, flags, s, aux);
@@ -3427,10 +3472,6 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
     hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1,
                        exact ? w.keys : nullptr, lists ? w.mk : nullptr, lists ? w.lcnt : nullptr, n);
   }
-  // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
-  int nl = n_lanes > 0 ? n_lanes : 1;
-  const int tiles = (B + 63) / 64;
-  if (nl > tiles) nl = tiles;
   if (nl == 1) {
     hipStream_t ls = n_lanes > 0 ? (hipStream_t)lanes[0] : s;
     hipEvent_t e = nullptr;
@@ -3450,7 +3491,6 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
     }
   } else {
     hipEvent_t fork, join[AA_MAX_LANES];
-    if (nl > AA_MAX_LANES) nl = AA_MAX_LANES;
     AA_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
     AA_TRY(hipEventRecord(fork, s));
     for (int i = 0; i < nl; ++i) {

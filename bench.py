@@ -86,8 +86,10 @@ def kernel_costs(B: int, T: int) -> dict:
         "k_enc_v4": ("mfma_x3", f["k_enc_v"] * B),  # + the fused avg-pool (not priced)
         "k_enc_v3": ("mfma_x3", f["k_enc_v"] * B),
         "k_enc_heads": ("mfma", f["k_enc_heads"] * B),
-        "k_enc_heads3": ("mfma_x3", f["k_enc_heads"] * B),
-        "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),
+        "k_gemm3(heads)": ("mfma_x3", f["k_enc_heads"] * B),
+        "k_gemm3(VWv)": ("mfma_x3", f["vwv"] * B),
+        "k_gemm3(x_g)": ("mfma_x3", f["xg"] * B),
+        "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),  # fp32-MFMA encoder builds (--enc-v3)
         "k_gemm_bias(x_g)": ("mfma", f["xg"] * B),
         "k_lstm": ("mfma_x3", f["k_lstm"] * B),
         "k_lstm_gemm": ("mfma_x3", f["k_lstm_gemm"] * B),
@@ -200,9 +202,9 @@ def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True, v_re
     atten_row = atten_bytes_per_row() - (0 if v_restream else 4 * P * H)
     parts = {
         "k_enc_v4": f["k_enc_v"] * B / PEAK_X3,
-        "k_enc_heads3": f["k_enc_heads"] * B / PEAK_X3,
-        "k_gemm_bias(VWv)": f["vwv"] * B / PEAK_FP32,
-        "k_gemm_bias(x_g)": f["xg"] * B / PEAK_FP32,
+        "k_gemm3(heads)": f["k_enc_heads"] * B / PEAK_X3,
+        "k_gemm3(VWv)": f["vwv"] * B / PEAK_X3,
+        "k_gemm3(x_g)": f["xg"] * B / PEAK_X3,
         "k_lstm": T * (f["k_lstm_gemm"] * B / PEAK_X3 + f["proj"] * B / PEAK_FP32),
         "k_atten": T * atten_row * B / PEAK_HBM,
         "k_vscreen": T * 2 * H * Vp * B / PEAK_BF16,
@@ -438,8 +440,8 @@ def main():
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
         lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
-        enc_names = ("k_avgpool", enc_name, "k_enc_heads" if args.enc_v3 else "k_enc_heads3", "k_gemm_bias(VWv)",
-                     "k_gemm_bias(x_g)")
+        enc_names = (("k_avgpool", enc_name, "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)") if args.enc_v3
+                     else ("k_avgpool", enc_name, "k_gemm3(heads)", "k_gemm3(VWv)", "k_gemm3(x_g)"))
         per = {k: [] for k in enc_names + (lstm, "k_atten", screen_name, rescore_name)}
         if not args.enc_v3:
             del per["k_avgpool"]  # fused into k_enc_v4 (its trace pair is empty)
