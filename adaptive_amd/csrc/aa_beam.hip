@@ -522,44 +522,38 @@ __global__ __launch_bounds__(512) void k_beam_select3(int K, int V, int Vp, int 
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float ocum[BEAM_MAX];
-    int ofin[BEAM_MAX];
-    for (int q = 0; q < K; ++q) {
-      ocum[q] = cum[b * K + q];
-      ofin[q] = fin[b * K + q];
-    }
-    float cv[BEAM_MAX * BEAM_MAX];
-    int cf[BEAM_MAX * BEAM_MAX];
-    int n = 0;
-    for (int q = 0; q < K; ++q) {
-      if (t == 0 && q > 0) continue;
-      if (ofin[q]) {
-        cv[n] = ocum[q];
-        cf[n++] = q * V + end_id;
-        continue;
-      }
-      for (int j = 0; j < K; ++j) {
-        const uint64_t key = s_top[q][j];
-        const float xv = key_value((uint32_t)(key >> 32));
-        cv[n] = ocum[q] + ((xv - s_mx[q]) - s_ls[q]);
-        cf[n++] = q * V + (int)key_token(key);
+  // merge on wave 0: lane q K + j holds beam q's j-th candidate (a finished beam: only j = 0, the
+  // token end_id at its unchanged score) as a key ordered by score, then by the smaller q V + v;
+  // K rounds of a wave max pick the survivors, each written by the lane that holds it.  (Per-thread
+  // candidate arrays indexed at run time lived in scratch memory: 12-20 us per launch.)
+  if (threadIdx.x < 64) {
+    const int q = lane / K, j = lane - q * K;
+    uint64_t key = 0;
+    int qfin = 0;
+    if (q < K && !(t == 0 && q > 0)) {
+      const float ocum = cum[b * K + q];
+      qfin = fin[b * K + q];
+      if (qfin) {
+        if (j == 0) key = argmax_key(ocum + 0.0f, q * V + end_id);
+      } else {
+        const uint64_t tk = s_top[q][j];
+        const float xv = key_value((uint32_t)(tk >> 32));
+        key = argmax_key((ocum + ((xv - s_mx[q]) - s_ls[q])) + 0.0f, q * V + (int)key_token(tk));
       }
     }
-    for (int j = 0; j < K; ++j) {
-      int bi = -1;
-      for (int i = 0; i < n; ++i) {
-        if (cf[i] < 0) continue;
-        if (bi < 0 || cv[i] > cv[bi] || (cv[i] == cv[bi] && cf[i] < cf[bi])) bi = i;
+    for (int jj = 0; jj < K; ++jj) {
+      const uint64_t best = wave_max_u64(key);
+      if (key == best && best != 0) {  // candidates are distinct (distinct q V + v)
+        const int cf = (int)(0xFFFFFFFFu - (uint32_t)best);
+        const int pk = cf / V, c = cf - pk * V, r = b * K + jj;
+        cum[r] = key_value((uint32_t)(best >> 32));
+        fin[r] = (qfin || c == end_id) ? 1 : 0;
+        tok[r] = c;
+        par[r] = b * K + pk;
+        htok[(int64_t)t * R + r] = c;
+        hpar[(int64_t)t * R + r] = pk;
+        key = 0;
       }
-      const int pk = cf[bi] / V, c = cf[bi] % V, r = b * K + j;
-      cum[r] = cv[bi];
-      fin[r] = (ofin[pk] || c == end_id) ? 1 : 0;
-      tok[r] = c;
-      par[r] = b * K + pk;
-      htok[(int64_t)t * R + r] = c;
-      hpar[(int64_t)t * R + r] = pk;
-      cf[bi] = -1;
     }
   }
 }

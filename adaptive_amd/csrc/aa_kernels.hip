@@ -1735,6 +1735,153 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   AA_TS(1, 4);
 }
 
+// k_atten5 for beam search: one workgroup per IMAGE runs the KB rows (beams) of that image, so the
+// image's V (100 KB) and VWv rows are loaded once instead of once per beam (the rows of an image are
+// adjacent: r = img KB + k).  Every row's arithmetic is k_atten5's, in the same order (bit-identical
+// alpha, beta, u); the rows' small loads are all issued up front, their phases share the barriers.
+template <int H, int KB>
+__global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new, const float* __restrict__ s_new,
+                                                 const float* __restrict__ part, const float* __restrict__ Vf,
+                                                 const float* __restrict__ VWv, const float* __restrict__ wh,
+                                                 float* __restrict__ alpha_out, int64_t alpha_ld,
+                                                 float* __restrict__ beta_out, int64_t beta_ld, float* __restrict__ u_out,
+                                                 uint16_t* __restrict__ ub_out, float* __restrict__ unorm,
+                                                 bf16x8* __restrict__ ub3_out) {
+  constexpr int DPT = H / 512, NT16 = H / 16, NG = NT16 / 4;
+  __shared__ float red[KB][4][128];
+  __shared__ float proj[KB][PART];
+  __shared__ float zs[KB][PP];
+  __shared__ float sh_alpha[KB][PP];
+  __shared__ float sh_beta[KB];
+  __shared__ float sh_norm[KB][8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int img = blockIdx.x, r0 = img * KB;
+  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
+  float pv[KB][NG];
+#pragma unroll
+  for (int r = 0; r < KB; ++r) {
+    const float* pp = part + ((int64_t)(r0 + r) * NT16 + grp) * PART + jpc;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) pv[r][i] = pp[(int64_t)4 * i * PART];
+  }
+  const int k = t >> 3, q = t & 7;
+  const int kc = k < P ? k : P - 1;
+  const float* vw = VWv + ((int64_t)img * P + kc) * PP;
+  float vwr[7], whr[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+    vwr[i] = vw[j];
+    whr[i] = q + 8 * i < P ? wh[j] : 0.f;
+  }
+  const float* vb = Vf + (int64_t)img * P * H;
+  float vv[DPT][P];
+#pragma unroll
+  for (int i = 0; i < DPT; ++i)
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
+  float hv[KB][DPT], sv[KB][DPT];
+#pragma unroll
+  for (int r = 0; r < KB; ++r)
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      hv[r][i] = h_new[(int64_t)(r0 + r) * H + t + 512 * i];
+      sv[r][i] = s_new[(int64_t)(r0 + r) * H + t + 512 * i];
+    }
+  // 1) projections
+#pragma unroll
+  for (int r = 0; r < KB; ++r) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) a += pv[r][i];
+    red[r][grp][jp] = a;
+  }
+  __syncthreads();
+  for (int e = t; e < KB * 2 * P; e += 512) {
+    const int r = e / (2 * P), j = e - r * (2 * P);
+    proj[r][j] = (red[r][0][j] + red[r][1][j]) + (red[r][2][j] + red[r][3][j]);
+  }
+  __syncthreads();
+  // 2) scores
+#pragma unroll
+  for (int r = 0; r < KB; ++r) {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+      const float x = (k < P ? vwr[i] : proj[r][P + j]) + proj[r][j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
+    }
+    z = z + __shfl_xor(z, 1, 64);
+    z = z + __shfl_xor(z, 2, 64);
+    z = z + __shfl_xor(z, 4, 64);
+    if (q == 0 && k <= P) zs[r][k] = z;
+  }
+  __syncthreads();
+  // 3) softmax: wave r for row r
+  if (w < KB) {
+    const int r = w, b = r0 + r;
+    const float z = lane < P ? zs[r][lane] : -INFINITY;
+    const float zsn = zs[r][P];
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float S = wave_sum(e);
+    const float a = e / S;
+    if (lane < P) {
+      sh_alpha[r][lane] = a;
+      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
+    }
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      const float beta = es / S2;
+      sh_beta[r] = beta;
+      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
+    }
+  }
+  __syncthreads();
+  // 4) context + u
+#pragma unroll
+  for (int r = 0; r < KB; ++r) {
+    const int b = r0 + r;
+    const float beta = sh_beta[r];
+    float nsq = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int d = t + 512 * i;
+      float c = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sh_alpha[r][kk], vv[i][kk], c);
+      const float chat = __builtin_fmaf(beta, sv[r][i], (1.f - beta) * c);
+      const float u = chat + hv[r][i];
+      nsq = __builtin_fmaf(u, u, nsq);
+      u_out[(int64_t)b * H + d] = u;
+      if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+      if (ub3_out) {
+        __bf16 x0, x1, x2;
+        split3(u, x0, x1, x2);
+        __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                              (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+        o[0] = x0;
+        o[64 * 8] = x1;
+        o[128 * 8] = x2;
+      }
+    }
+    if (unorm) {
+      nsq = wave_sum(nsq);
+      if (lane == 0) sh_norm[r][w] = nsq;
+    }
+  }
+  if (unorm) {
+    __syncthreads();
+    if (t < KB)
+      unorm[r0 + t] = sqrtf(((sh_norm[t][0] + sh_norm[t][1]) + (sh_norm[t][2] + sh_norm[t][3])) +
+                            ((sh_norm[t][4] + sh_norm[t][5]) + (sh_norm[t][6] + sh_norm[t][7]))) * 1.00001f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a
 // 128x128 tile, then per (row, 32-column granule g) with the granule's bound E (see CEPS):
@@ -3192,7 +3339,10 @@ static void lstm_cell_launch(const Layout& L, const MP& p, int B, const int64_t*
 #undef AA_CELL
 }
 
-// Attention for one step (kdiv rows per image: beam search)
+// Attention for one step (kdiv rows per image: beam search; k_atten5b runs an image's rows together)
+#ifndef AA_ATTEN_BEAM
+#define AA_ATTEN_BEAM 1
+#endif
 static void atten_launch(const Layout& L, const MP& p, int B, const float* V, const float* vwv, const float* h_out,
                          float* s_buf, float* part, float* u, uint16_t* ub, float* unorm, float* alpha,
                          int64_t alpha_ld, float* beta, int64_t beta_ld, hipStream_t s, int kdiv = 1,
@@ -3204,6 +3354,18 @@ static void atten_launch(const Layout& L, const MP& p, int B, const float* V, co
 #define AA_ATTEN5(H_)                                                                                      \
   hipLaunchKernelGGL(k_atten5<H_>, dim3(B), dim3(512), 0, s, B, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
                      alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+#define AA_ATTEN5B(KB_)                                                                                    \
+  hipLaunchKernelGGL((k_atten5b<512, KB_>), dim3(B / KB_), dim3(512), 0, s, h_out, s_buf, part, V, vwv, p.wh, alpha, \
+                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+  if (H == 512 && kdiv >= 2 && kdiv <= 5 && B % kdiv == 0 && AA_ATTEN_BEAM) {  // beam: one workgroup per image
+    switch (kdiv) {
+      case 2: AA_ATTEN5B(2); break;
+      case 3: AA_ATTEN5B(3); break;
+      case 4: AA_ATTEN5B(4); break;
+      default: AA_ATTEN5B(5); break;
+    }
+    return;
+  }
   switch (H) {
     case 256: AA_ATTEN(1); break;
     case 512: AA_ATTEN5(512); break;
@@ -3212,6 +3374,7 @@ static void atten_launch(const Layout& L, const MP& p, int B, const float* V, co
   }
 #undef AA_ATTEN
 #undef AA_ATTEN5
+#undef AA_ATTEN5B
 }
 
 // LSTM + attention for one step (fused LSTM kernel)

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Bitwise A/B of two library builds on one decode (GPU box): run once per build with AA_LIB_PATH
+set, dumping the outputs; then compare the dumps.
+    AA_LIB_PATH=a.so python tools/ab_bits.py dump gpurun_out/a.npz [--beam K] [--batch B]
+    AA_LIB_PATH=b.so python tools/ab_bits.py dump gpurun_out/b.npz ...
+    python tools/ab_bits.py cmp gpurun_out/a.npz gpurun_out/b.npz"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def dump(path, beam, batch, T, fast):
+    import torch
+    from adaptive_amd import Config, Encoder2Decoder
+    from adaptive_amd.adaptive_attention import synthetic_features
+    m = Encoder2Decoder(Config()).to("cuda:0")
+    m.load_synthetic(123)
+    feats = synthetic_features(batch, "cuda:0", seed=0)
+    if beam:
+        out = m.beam_search(feats, max_len=T, beam_size=beam, fast=fast)
+        names = ("ids", "alpha", "beta", "seqs", "scores")
+    else:
+        out = m.sampler(feats, max_len=T)
+        names = ("ids", "alpha", "beta")
+    torch.cuda.synchronize()
+    np.savez(path, **{n: o.cpu().numpy() for n, o in zip(names, out)})
+    print("dumped", path, {n: o.shape for n, o in zip(names, out)})
+
+
+def cmp(a, b):
+    x, y = np.load(a), np.load(b)
+    ok = True
+    for n in x.files:
+        same = x[n].tobytes() == y[n].tobytes()
+        ok &= same
+        print(n, "bit-identical" if same else f"DIFFERS (max |d| {np.abs(x[n].astype(np.float64) - y[n]).max():.3g})")
+    print("ALL BIT-IDENTICAL" if ok else "DIFFERENT")
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=("dump", "cmp"))
+    ap.add_argument("files", nargs="+")
+    ap.add_argument("--beam", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--T", type=int, default=20)
+    ap.add_argument("--fast", action="store_true")
+    a = ap.parse_args()
+    if a.mode == "dump":
+        dump(a.files[0], a.beam, a.batch, a.T, a.fast)
+    else:
+        sys.exit(cmp(*a.files))
