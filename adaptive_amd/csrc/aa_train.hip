@@ -479,136 +479,179 @@ __global__ void k_tr_prow(const int* __restrict__ len, int B, int T, int* __rest
 // ---------------------------------------------------------------------------------------------
 // backward pieces
 // ---------------------------------------------------------------------------------------------
-// Atten backward, one workgroup per (image b, step group g) over the steps t in
-// [g TS, min((g+1) TS, len[b])) in order (rows t >= len[b] carry no loss gradient), 256 threads,
-// HPT = H / 256 columns per thread.  With more than one group each group writes its own partial
-// dV / dVWv / dwh (strides sV, sVW, swh) and k_sum_groups adds them in group order.
-// In: dU (= dc_hat; u = c_hat + h also gives dh = dU directly), alpha, beta, ctx (c_t), S, PG,
-// PS, VWv, V, w_h.  Out per row: dS = beta dU, dPG, dPS (pitch PP); per image: dV[b] (+)= sum_t
-// alpha_t (x) dc_t, dVWv[b] = sum_t dcontent_v, dwh_part[b][j].
-//   beta = softmax_50([z; z_s])[49]:  dz_k += -dbeta beta (1 - beta) alpha_k, dz_s = dbeta beta (1 - beta)
-//   alpha = softmax_49(z):           dz_k += alpha_k (dalpha_k - <alpha, dalpha>)
+// Atten backward in two passes.  Nothing in it is sequential over t (dU for every step is known
+// once the vocab backward has run); only the per-image sums over t are, so:
+// k_tr_atb_row: one workgroup per row r = t B + b (t < len[b]; rows past a caption's length carry
+//   no loss gradient), 256 threads, HPT = H / 256 columns per thread.  In: dU (= dc_hat; u = c_hat +
+//   h also gives dh = dU directly), alpha, beta, ctx (c_t), S, PG, PS, VWv, V, w_h.  Out per row:
+//   dS = beta dU, dPG, dPS (pitch PP), and for the per-image pass dz (pitch PP) and the row's w_h
+//   gradient term dwr[j] = sum_k dz_k tanh_kj + dz_s tanh_s,j.
+//     beta = softmax_50([z; z_s])[49]:  dz_k += -dbeta beta (1 - beta) alpha_k, dz_s = dbeta beta (1 - beta)
+//     alpha = softmax_49(z):           dz_k += alpha_k (dalpha_k - <alpha, dalpha>)
+// k_tr_atb_img: one workgroup per image: dV[b] = sum_t alpha_t (x) dc_t, dVWv[b] = sum_t dcontent_v,t
+//   (tanh recomputed from VWv and PG), dwh_part[b] = sum_t dwr_t, each summed over t in the step
+//   groups of atb_groups, chained within a group and the group sums added in group order -- the
+//   arithmetic of the one-pass kernel this replaced (a workgroup per (image, step group), 237 us at
+//   B = 128, T = 18), so the gradients are bit-identical to it.
 template <int HPT>
-__global__ __launch_bounds__(256) void k_tr_atten_bwd(int B, int TS, int64_t sV, int64_t sVW, int64_t swh,
-                                                      const int* __restrict__ len, const float* __restrict__ dU,
-                                                      const float* __restrict__ alpha, const float* __restrict__ beta,
-                                                      const float* __restrict__ ctx, const float* __restrict__ S,
-                                                      const float* __restrict__ PG, const float* __restrict__ PS,
-                                                      const float* __restrict__ VWv, const float* __restrict__ Vf,
-                                                      const float* __restrict__ wh, float* __restrict__ dS,
-                                                      float* __restrict__ dPG, float* __restrict__ dPS,
-                                                      float* __restrict__ dV, float* __restrict__ dVWv,
-                                                      float* __restrict__ dwh_part) {
+__global__ __launch_bounds__(256) void k_tr_atb_row(int B, const int* __restrict__ len, const float* __restrict__ dU,
+                                                    const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                    const float* __restrict__ ctx, const float* __restrict__ S,
+                                                    const float* __restrict__ PG, const float* __restrict__ PS,
+                                                    const float* __restrict__ VWv, const float* __restrict__ Vf,
+                                                    const float* __restrict__ wh, float* __restrict__ dS,
+                                                    float* __restrict__ dPG, float* __restrict__ dPS,
+                                                    float* __restrict__ dz_out, float* __restrict__ dwr) {
   constexpr int H = 256 * HPT;
   __shared__ float s_al[PP], s_da[PP], s_dz[PP], s_red[4], s_dzs;
   __shared__ float s_dc[H];
   __shared__ float s_cv[P * P], s_tz[P * P];
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = blockIdx.x, b = r % B, tt = r / B;
+  if (tt >= len[b]) return;  // uniform over the workgroup
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float* vb = Vf + (int64_t)b * P * H;
-  float dv_acc[HPT][P];
-#pragma unroll
-  for (int i = 0; i < HPT; ++i)
-#pragma unroll
-    for (int k = 0; k < P; ++k) dv_acc[i][k] = 0.f;
-  float dvwv_acc[10];  // thread owns entries e = t + 256 i of dVWv[b] (49 x 49)
-#pragma unroll
-  for (int i = 0; i < 10; ++i) dvwv_acc[i] = 0.f;
-  float dwh_acc = 0.f;
   const float whj = t < P ? wh[t] : 0.f;
-  const int g = blockIdx.y, nt = min(len[b], (g + 1) * TS);
-  dV += g * sV;
-  dVWv += g * sVW;
-  dwh_part += g * swh;
-  for (int tt = g * TS; tt < nt; ++tt) {
-    const int r = tt * B + b;
-    const float be = beta[r];
-    float part = 0.f;
-#pragma unroll
-    for (int i = 0; i < HPT; ++i) {
-      const int d = t + 256 * i;
-      const float du = dU[(int64_t)r * H + d];
-      part += du * (S[(int64_t)r * H + d] - ctx[(int64_t)r * H + d]);
-      dS[(int64_t)r * H + d] = be * du;
-      s_dc[d] = (1.f - be) * du;
-    }
-    part = wave_sum(part);
-    if (lane == 0) s_red[w] = part;
-    if (t < PP) s_al[t] = t < P ? alpha[(int64_t)r * PP + t] : 0.f;
-    __syncthreads();
-    const float dbeta = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-    for (int k = w; k < P; k += 4) {  // dalpha_k = dc . V_k
-      float a = 0.f;
-      for (int d = lane; d < H; d += 64) a = __builtin_fmaf(s_dc[d], vb[(int64_t)k * H + d], a);
-      a = wave_sum(a);
-      if (lane == 0) s_da[k] = a;
-    }
-#pragma unroll
-    for (int i = 0; i < HPT; ++i) {  // dV[b][k][d] += alpha_k dc_d
-      const float dcd = s_dc[t + 256 * i];
-#pragma unroll
-      for (int k = 0; k < P; ++k) dv_acc[i][k] = __builtin_fmaf(s_al[k], dcd, dv_acc[i][k]);
-    }
-    __syncthreads();
-    if (w == 0) {
-      const float a = lane < P ? s_al[lane] : 0.f;
-      const float da = lane < P ? s_da[lane] : 0.f;
-      const float dot = wave_sum(a * da);
-      const float dzb = dbeta * be * (1.f - be);
-      if (lane < P) s_dz[lane] = a * (da - dot) - dzb * a;
-      if (lane == 0) s_dzs = dzb;
-    }
-    __syncthreads();
-    // content_v[k][j] = VWv[b][k][j] + PG[j]: entries e = k * 49 + j spread over the threads
-    const float* pgr = PG + (int64_t)r * PP;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int e = t + 256 * i;
-      if (e < P * P) {
-        const int k = e / P, j = e - k * P;
-        const float th = tanhf(VWv[((int64_t)b * P + k) * PP + j] + pgr[j]);
-        const float dcv = s_dz[k] * wh[j] * (1.f - th * th);
-        dvwv_acc[i] += dcv;
-        s_cv[e] = dcv;
-        s_tz[e] = s_dz[k] * th;
-      }
-    }
-    __syncthreads();
-    if (t < P) {  // column j: dPG[j] = sum_k dcv[k][j] + dcs[j]; dwh[j] += sum_k dz_k tanh + dz_s tanh_s
-      const int j = t;
-      float sdcv = 0.f, sdw = 0.f;
-      for (int k = 0; k < P; ++k) {
-        sdcv += s_cv[k * P + j];
-        sdw += s_tz[k * P + j];
-      }
-      const float ths = tanhf(PS[(int64_t)r * PP + j] + pgr[j]);
-      const float dcs = s_dzs * whj * (1.f - ths * ths);
-      dPS[(int64_t)r * PP + j] = dcs;
-      dPG[(int64_t)r * PP + j] = sdcv + dcs;
-      dwh_acc += sdw + s_dzs * ths;
-    }
-    __syncthreads();
-  }
+  const float be = beta[r];
+  float part = 0.f;
 #pragma unroll
   for (int i = 0; i < HPT; ++i) {
     const int d = t + 256 * i;
+    const float du = dU[(int64_t)r * H + d];
+    part += du * (S[(int64_t)r * H + d] - ctx[(int64_t)r * H + d]);
+    dS[(int64_t)r * H + d] = be * du;
+    s_dc[d] = (1.f - be) * du;
+  }
+  part = wave_sum(part);
+  if (lane == 0) s_red[w] = part;
+  if (t < PP) s_al[t] = t < P ? alpha[(int64_t)r * PP + t] : 0.f;
+  __syncthreads();
+  const float dbeta = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+  for (int k = w; k < P; k += 4) {  // dalpha_k = dc . V_k
+    float a = 0.f;
+    for (int d = lane; d < H; d += 64) a = __builtin_fmaf(s_dc[d], vb[(int64_t)k * H + d], a);
+    a = wave_sum(a);
+    if (lane == 0) s_da[k] = a;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const float a = lane < P ? s_al[lane] : 0.f;
+    const float da = lane < P ? s_da[lane] : 0.f;
+    const float dot = wave_sum(a * da);
+    const float dzb = dbeta * be * (1.f - be);
+    const float dz = a * (da - dot) - dzb * a;
+    if (lane < P) {
+      s_dz[lane] = dz;
+      dz_out[(int64_t)r * PP + lane] = dz;
+    }
+    if (lane == 0) s_dzs = dzb;
+  }
+  __syncthreads();
+  // content_v[k][j] = VWv[b][k][j] + PG[j]: entries e = k * 49 + j spread over the threads
+  const float* pgr = PG + (int64_t)r * PP;
 #pragma unroll
-    for (int k = 0; k < P; ++k) dV[((int64_t)b * P + k) * H + d] = dv_acc[i][k];
+  for (int i = 0; i < 10; ++i) {
+    const int e = t + 256 * i;
+    if (e < P * P) {
+      const int k = e / P, j = e - k * P;
+      const float th = tanhf(VWv[((int64_t)b * P + k) * PP + j] + pgr[j]);
+      s_cv[e] = s_dz[k] * wh[j] * (1.f - th * th);
+      s_tz[e] = s_dz[k] * th;
+    }
+  }
+  __syncthreads();
+  if (t < P) {  // column j: dPG[j] = sum_k dcv[k][j] + dcs[j]; dwr[j] = sum_k dz_k tanh + dz_s tanh_s
+    const int j = t;
+    float sdcv = 0.f, sdw = 0.f;
+    for (int k = 0; k < P; ++k) {
+      sdcv += s_cv[k * P + j];
+      sdw += s_tz[k * P + j];
+    }
+    const float ths = tanhf(PS[(int64_t)r * PP + j] + pgr[j]);
+    const float dcs = s_dzs * whj * (1.f - ths * ths);
+    dPS[(int64_t)r * PP + j] = dcs;
+    dPG[(int64_t)r * PP + j] = sdcv + dcs;
+    dwr[(int64_t)r * PP + j] = sdw + s_dzs * ths;
+  }
+}
+
+// grid (B, HPT + 1): y < HPT -> dV columns 256 y + t; y = HPT -> dVWv and dwh_part
+template <int HPT>
+__global__ __launch_bounds__(256) void k_tr_atb_img(int B, int TS, int G, const int* __restrict__ len,
+                                                    const float* __restrict__ dU, const float* __restrict__ alpha,
+                                                    const float* __restrict__ beta, const float* __restrict__ PG,
+                                                    const float* __restrict__ VWv, const float* __restrict__ wh,
+                                                    const float* __restrict__ dz_in, const float* __restrict__ dwr,
+                                                    float* __restrict__ dV, float* __restrict__ dVWv,
+                                                    float* __restrict__ dwh_part) {
+  constexpr int H = 256 * HPT;
+  __shared__ float s_al[PP], s_dz[PP], s_pg[PP];
+  const int b = blockIdx.x, role = blockIdx.y, t = threadIdx.x, n = len[b];
+  if (role < HPT) {  // dV[b][k][d] = sum_t alpha_t,k dc_t,d
+    const int d = t + 256 * role;
+    float tot[P], acc[P];
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) acc[k] = 0.f;
+      const int nt = min(n, (g + 1) * TS);
+      for (int tt = g * TS; tt < nt; ++tt) {
+        const int r = tt * B + b;
+        __syncthreads();  // the previous step's alpha was read
+        if (t < PP) s_al[t] = t < P ? alpha[(int64_t)r * PP + t] : 0.f;
+        const float dc = (1.f - beta[r]) * dU[(int64_t)r * H + d];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P; ++k) acc[k] = __builtin_fmaf(s_al[k], dc, acc[k]);
+      }
+      // group sums added in group order (as the group partials were summed: the first taken as is)
+#pragma unroll
+      for (int k = 0; k < P; ++k) tot[k] = g == 0 ? acc[k] : tot[k] + acc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) dV[((int64_t)b * P + k) * H + d] = tot[k];
+    return;
+  }
+  float dvwv_tot[10], dvwv_acc[10], vwv[10], whv[10];
+  float dwh_tot = 0.f, dwh_acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int e = t + 256 * i, ec = e < P * P ? e : 0, k = ec / P, j = ec - k * P;
+    vwv[i] = VWv[((int64_t)b * P + k) * PP + j];
+    whv[i] = wh[j];
+  }
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) dvwv_acc[i] = 0.f;
+    dwh_acc = 0.f;
+    const int nt = min(n, (g + 1) * TS);
+    for (int tt = g * TS; tt < nt; ++tt) {
+      const int r = tt * B + b;
+      __syncthreads();
+      if (t < PP) {
+        s_dz[t] = t < P ? dz_in[(int64_t)r * PP + t] : 0.f;
+        s_pg[t] = t < P ? PG[(int64_t)r * PP + t] : 0.f;
+      }
+      if (t < P) dwh_acc += dwr[(int64_t)r * PP + t];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const int e = t + 256 * i;
+        if (e < P * P) {
+          const int k = e / P, j = e - k * P;
+          const float th = tanhf(vwv[i] + s_pg[j]);
+          dvwv_acc[i] += s_dz[k] * whv[i] * (1.f - th * th);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) dvwv_tot[i] = g == 0 ? dvwv_acc[i] : dvwv_tot[i] + dvwv_acc[i];
+    dwh_tot = g == 0 ? dwh_acc : dwh_tot + dwh_acc;
   }
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     const int e = t + 256 * i;
-    if (e < P * P) dVWv[((int64_t)b * P + e / P) * PP + e % P] = dvwv_acc[i];
+    if (e < P * P) dVWv[((int64_t)b * P + e / P) * PP + e % P] = dvwv_tot[i];
   }
-  if (t < P) dwh_part[(int64_t)b * PP + t] = dwh_acc;
-}
-
-// out[i] = sum over g of parts[g n + i], in g order
-__global__ void k_sum_groups(const float* __restrict__ parts, int G, int64_t n, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float v = parts[i];
-  for (int g = 1; g < G; ++g) v += parts[g * n + i];
-  out[i] = v;
+  if (t < P) dwh_part[(int64_t)b * PP + t] = dwh_tot;
 }
 
 // copy a [rows][cols] matrix into pitch `pitch` (zero padding)
@@ -673,26 +716,25 @@ __device__ __forceinline__ int tok_of(const int64_t* tok, int tld, int B, int V,
   int64_t tk = tok[(int64_t)b * tld + t];
   return (int)(tk < 0 ? 0 : (tk >= V ? V - 1 : tk));
 }
-constexpr int TOK_CH = 4096;  // tokens staged per LDS pass
-__global__ void k_tok_rank(const int64_t* __restrict__ tok, int tld, int B, int R, int V, int* __restrict__ rank,
-                           int* __restrict__ count, int* __restrict__ before_tok) {
-  __shared__ int st[TOK_CH];
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int v = r < R ? tok_of(tok, tld, B, V, r) : -1;
+// one wave per row r: the 64 lanes stride over all R rows, counting (ballot + popcount) the rows
+// with r's token before r, in total, and the rows with a smaller token (a thread per row looping
+// over all R rows ran on R / 256 workgroups: 69 us at R = 2304)
+__global__ __launch_bounds__(256) void k_tok_rank(const int64_t* __restrict__ tok, int tld, int B, int R, int V,
+                                                  int* __restrict__ rank, int* __restrict__ count,
+                                                  int* __restrict__ before_tok) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;  // wave-uniform
+  const int v = tok_of(tok, tld, B, V, r);
   int before = 0, total = 0, smaller = 0;
-  for (int c0 = 0; c0 < R; c0 += TOK_CH) {
-    const int n = R - c0 < TOK_CH ? R - c0 : TOK_CH;
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) st[i] = tok_of(tok, tld, B, V, c0 + i);
-    __syncthreads();
-    for (int i = 0; i < n; ++i) {
-      const int u = st[i];
-      total += u == v;
-      before += (u == v) && (c0 + i < r);
-      smaller += u < v;
-    }
+  for (int i0 = 0; i0 < R; i0 += 64) {
+    const int i = i0 + lane;
+    const int u = i < R ? tok_of(tok, tld, B, V, i) : -1;
+    const bool same = i < R && u == v;
+    total += __popcll(__ballot(same));
+    before += __popcll(__ballot(same && i < r));
+    smaller += __popcll(__ballot(i < R && u < v));
   }
-  if (r < R) {
+  if (lane == 0) {
     rank[r] = before;
     count[r] = total;
     before_tok[r] = smaller;
@@ -778,11 +820,12 @@ struct TrainWS {
   // backward scratch
   float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
   float *dA, *dag;  // d(features) pieces: through V [B*49][C] and through a_g [B][C]
-  float *pV, *pVWv, *pwh;  // per-step-group partials of k_tr_atten_bwd (atb_groups > 1)
+  float *dz, *dwr;  // per-row dz and w_h-gradient terms of k_tr_atb_row, summed per image by k_tr_atb_img
   int *trank, *tcount, *torder, *tsmall;
 };
 
-// step groups of k_tr_atten_bwd: enough (image, group) workgroups to cover the chip at small B
+// step groups of the attention backward's per-image sums over t (k_tr_atb_img; they were the
+// (image, group) workgroups of the one-pass kernel, sized to cover the chip at small B)
 static void atb_groups(int B, int T, int* G, int* TS) {
   int g = B > 0 ? (512 + B - 1) / B : 1;
   g = g < T ? g : T;
@@ -841,12 +884,8 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.tcount = c.take<int>(R);
   w.torder = c.take<int>(R);
   w.tsmall = c.take<int>(R);
-  int G, TS;
-  atb_groups(B, T, &G, &TS);
-  const size_t np = G > 1 ? (size_t)G : 0;
-  w.pV = c.take<float>(np * B * P_ * H);
-  w.pVWv = c.take<float>(np * B * P_ * PP_);
-  w.pwh = c.take<float>(np * B * PP_);
+  w.dz = c.take<float>(R * PP_);
+  w.dwr = c.take<float>(R * PP_);
   *bytes = c.off;
   return w;
 }
@@ -1030,13 +1069,11 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   AA_TRY(hipMemsetAsync(s.dPS, 0, sizeof(float) * (size_t)R * PP, st));
   int G, TS;
   atb_groups(B, T, &G, &TS);
-  const bool grouped = G > 1;
-  const int64_t nV = (int64_t)B * P * H, nVW = (int64_t)B * P * PP, nwh = (int64_t)B * PP;
 #define AA_ATB(HPT_)                                                                                          \
-  hipLaunchKernelGGL(k_tr_atten_bwd<HPT_>, dim3(B, G), dim3(256), 0, st, B, TS, grouped ? nV : 0,              \
-                     grouped ? nVW : 0, grouped ? nwh : 0, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, s.PG, s.PS, \
-                     s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, grouped ? s.pV : s.dV,                   \
-                     grouped ? s.pVWv : s.dVWv, grouped ? s.pwh : s.dwh)
+  hipLaunchKernelGGL(k_tr_atb_row<HPT_>, dim3(R), dim3(256), 0, st, B, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, \
+                     s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, s.dz, s.dwr);                 \
+  hipLaunchKernelGGL(k_tr_atb_img<HPT_>, dim3(B, HPT_ + 1), dim3(256), 0, st, B, TS, G, lengths, s.dU, s.alpha, s.beta, s.PG, \
+                     s.VWv, w->att_affine_h_w, s.dz, s.dwr, s.dV, s.dVWv, s.dwh)
   switch (H / 256) {
     case 1: AA_ATB(1); break;
     case 2: AA_ATB(2); break;
@@ -1044,11 +1081,6 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     default: AA_ATB(4); break;
   }
 #undef AA_ATB
-  if (grouped) {
-    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nV)), dim3(256), 0, st, s.pV, G, nV, s.dV);
-    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nVW)), dim3(256), 0, st, s.pVWv, G, nVW, s.dVWv);
-    hipLaunchKernelGGL(k_sum_groups, dim3(nblk(nwh)), dim3(256), 0, st, s.pwh, G, nwh, s.dwh);
-  }
   AA_TRY(hipMemcpyAsync(s.dH, s.dU, sizeof(float) * RH, hipMemcpyDeviceToDevice, st));  // u = c_hat + h
   tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
   tgemm(gc, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
@@ -1086,7 +1118,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   tgemm(gc, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
   // x_t = [embed(tok); v_g] (baseline_attention.py:151-154)
   AA_TRY(hipMemsetAsync(GRAD(embed_w), 0, sizeof(float) * (size_t)V * E, st));
-  hipLaunchKernelGGL(k_tok_rank, dim3(nblk(R)), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.trank, s.tcount,
+  hipLaunchKernelGGL(k_tok_rank, dim3((R + 3) / 4), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.trank, s.tcount,
                      s.tsmall);
   hipLaunchKernelGGL(k_tok_place, dim3(nblk(R)), dim3(256), 0, st, R, s.trank, s.tsmall, s.torder);
   hipLaunchKernelGGL(k_tr_embed_bwd, dim3(R), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.torder, s.trank, s.tcount,
