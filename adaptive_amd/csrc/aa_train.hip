@@ -273,6 +273,10 @@ __global__ void k_tgemm_reduce(TG g) {
   *dst = g.accumulate ? *dst + v : v;
 }
 
+// k_tgemm's split-K bound (floats of partials): its split counts, and so its fp32 sums, as before
+// the scratch grew for k_bgemm
+constexpr size_t TG_SPLIT_CAP = (size_t)4 << 20;
+
 // launch context of a training call: stream + split-K scratch carved from its workspace
 struct GemmCtx {
   hipStream_t s;
@@ -302,7 +306,7 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
     splits = small ? (256 + tiles - 1) / tiles : (1024 + tiles - 1) / tiles;
     const int kmax = K / (small ? 128 : 512);
     if (splits > kmax) splits = kmax;
-    const size_t capsp = gc.cap / ((size_t)M * N);
+    const size_t capsp = (gc.cap < TG_SPLIT_CAP ? gc.cap : TG_SPLIT_CAP) / ((size_t)M * N);
     if ((size_t)splits > capsp) splits = (int)capsp;
     if (splits < 2) splits = 1;
   }
@@ -323,6 +327,218 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
   return splits;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The four large GEMMs of a bf16 step (vocab forward, dU = dS W_m, dW_m = dS^T U, dW_a = dV^T A) on
+// pre-packed bf16 operands: k_tgemm converted fp32 operands while staging 64 x 64 tiles (16 FLOP
+// per byte through the CU, 6-10 % of the bf16 peak on these shapes).  Here both operands are bf16,
+// row-major and K-contiguous ("NT": C[m][n] = sum_k A[m][k] B[n][k]), K a multiple of 64 with
+// zero padding, produced by the k_pk_* kernels below (RNE, the same rounding k_tgemm<true> applies
+// while staging), and a workgroup computes a 128 x 128 tile (four waves of 64 x 64 = 2 x 2
+// v_mfma_f32_32x32x16_bf16 blocks), 64-deep K steps double-buffered in LDS (144-B rows:
+// conflict-free 16-B fragment reads and staging stores).  Split-K partials go through
+// k_tgemm_reduce (fixed split order), so a step stays deterministic.
+// ---------------------------------------------------------------------------------------------
+constexpr int BG_T = 128, BG_KS = 64, BG_LD = BG_KS + 8;
+struct BG {
+  int M, N, K;
+  const __bf16* A;
+  int64_t lda;
+  const __bf16* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  const int* crow;
+  const float* bias;
+  int accumulate, splits, kper;
+  float* part;
+};
+__global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BG_T * BG_LD];
+  const int tilesN = (g.N + BG_T - 1) / BG_T;
+  const int split = blockIdx.x % g.splits, tile = blockIdx.x / g.splits;
+  const int mt = tile / tilesN, nt = tile % tilesN;
+  const int m0 = mt * BG_T, n0 = nt * BG_T;
+  const int kbeg = split * g.kper, kend = kbeg + g.kper < g.K ? kbeg + g.kper : g.K;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  // staging: 128 rows x 64 k per operand and step = 1024 16-B pieces, four per thread: piece
+  // q = t + 256 i -> row q >> 3, k 8 (q & 7) (8 lanes per 128-B row: coalesced loads, conflict-free
+  // ds_write_b128); rows past M / N are clamped (never stored)
+  const __bf16* pa[4];
+  const __bf16* pb[4];
+  int so[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = t + 256 * i, r = q >> 3, kq = (q & 7) * 8;
+    const int m = m0 + r < g.M ? m0 + r : g.M - 1, n = n0 + r < g.N ? n0 + r : g.N - 1;
+    pa[i] = g.A + (int64_t)m * g.lda + kq;
+    pb[i] = g.B + (int64_t)n * g.ldb + kq;
+    so[i] = r * BG_LD + kq;
+  }
+  bf16x8 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i] = *reinterpret_cast<const bf16x8*>(pa[i] + k0);
+      rb[i] = *reinterpret_cast<const bf16x8*>(pb[i] + k0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<bf16x8*>(&lds[buf][0][so[i]]) = ra[i];
+      *reinterpret_cast<bf16x8*>(&lds[buf][1][so[i]]) = rb[i];
+    }
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
+  const int nk = (kend - kbeg) / BG_KS;
+  gload(kbeg);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * BG_KS);
+    const __bf16* As = lds[buf][0];
+    const __bf16* Bs = lds[buf][1];
+#pragma unroll
+    for (int kb = 0; kb < BG_KS / 16; ++kb) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + x * 32 + li) * BG_LD + 16 * kb + 8 * lh);
+#pragma unroll
+      for (int y = 0; y < 2; ++y) b[y] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + y * 32 + li) * BG_LD + 16 * kb + 8 * lh);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x], b[y], acc[x][y], 0, 0, 0);
+    }
+    if (ks + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int y = 0; y < 2; ++y) {
+    const int col = n0 + wn * 64 + y * 32 + li;
+    if (col >= g.N) continue;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + x * 32 + acc_row(r, lane);
+        if (m >= g.M) continue;
+        if (g.splits > 1) {
+          g.part[(int64_t)split * g.M * g.N + (int64_t)m * g.N + col] = acc[x][y][r];
+        } else {
+          const float v = acc[x][y][r] + bv;
+          float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
+          *dst = g.accumulate ? *dst + v : v;
+        }
+      }
+  }
+}
+
+// dst[r][k] = bf16(src[map ? map[r] : r][k]) for k < cols, 0 up to Kp (a multiple of 8): 8 per thread,
+// as two 16-B loads when the source rows allow (vec: lds % 4 == 0, cols % 8 == 0, 16-B aligned base)
+__global__ void k_pk_rows(const float* __restrict__ src, int64_t lds, const int* __restrict__ map, int rows, int cols,
+                          __bf16* __restrict__ dst, int Kp, int vec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = Kp / 8;
+  if (i >= (int64_t)rows * per) return;
+  const int r = (int)(i / per), k0 = (int)(i % per) * 8;
+  const float* sr = src + (int64_t)(map ? map[r] : r) * lds;
+  bf16x8 v;
+  if (vec && k0 < cols) {
+    const float4 x = *reinterpret_cast<const float4*>(sr + k0), y = *reinterpret_cast<const float4*>(sr + k0 + 4);
+    v[0] = (__bf16)x.x; v[1] = (__bf16)x.y; v[2] = (__bf16)x.z; v[3] = (__bf16)x.w;
+    v[4] = (__bf16)y.x; v[5] = (__bf16)y.y; v[6] = (__bf16)y.z; v[7] = (__bf16)y.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)(k0 + j < cols ? sr[k0 + j] : 0.f);
+  }
+  *reinterpret_cast<bf16x8*>(dst + (int64_t)r * Kp + k0) = v;
+}
+
+// transpose: dst[c][r] = bf16(src[r lds + c]) for r < rows, 0 for rows <= r < Kp; dst has cols rows
+// of Kp.  64 x 64 tiles through LDS (reads along c, writes along r, both coalesced).  S: float or
+// __bf16 (a bf16 source is already rounded: the same values)
+template <class S>
+__global__ __launch_bounds__(256) void k_pk_trans(const S* __restrict__ src, int64_t lds, int rows, int cols,
+                                                  __bf16* __restrict__ dst, int Kp) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64, t = threadIdx.x;
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int rr = i / 64, cc = i % 64, r = r0 + rr, c = c0 + cc;
+    tile[rr][cc] = (r < rows && c < cols) ? (float)src[(int64_t)r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int cc = i / 64, rr = i % 64, c = c0 + cc, r = r0 + rr;
+    if (c < cols && r < Kp) dst[(int64_t)c * Kp + r] = (__bf16)tile[rr][cc];
+  }
+}
+
+// the NCHW feature map as the K-contiguous operand of dW_a = dV^T A: dst[c][b 49 + p] = feats[b][c][p],
+// zero for rows >= B 49 up to Kp; 8 consecutive rows per thread (one 16-B store)
+__global__ void k_pk_feats(const float* __restrict__ feats, int B, int C, __bf16* __restrict__ dst, int Kp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = Kp / 8;
+  if (i >= (int64_t)C * per) return;
+  const int c = (int)(i / per), row0 = (int)(i % per) * 8;
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = row0 + j;
+    float x = 0.f;
+    if (row < B * P) {
+      const int b = row / P, p = row - b * P;
+      x = feats[((int64_t)b * C + c) * P + p];
+    }
+    v[j] = (__bf16)x;
+  }
+  *reinterpret_cast<bf16x8*>(dst + (int64_t)c * Kp + row0) = v;
+}
+
+// C[M,N] (+)= A B^T (+ bias) on k_bgemm; K a multiple of 64.  Fewer than 512 tiles: split K to
+// ~1024 workgroups (bounded by the split scratch), partials reduced by k_tgemm_reduce in split order.
+static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb,
+                  float* C, int64_t ldc, const float* bias = nullptr, const int* crow = nullptr, int accumulate = 0) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  const int tiles = ((M + BG_T - 1) / BG_T) * ((N + BG_T - 1) / BG_T), ksteps = K / BG_KS;
+  int splits = tiles >= 512 ? 1 : (1024 + tiles - 1) / tiles;
+  if (splits > ksteps) splits = ksteps;
+  const size_t capsp = gc.split ? gc.cap / ((size_t)M * N) : 1;
+  if ((size_t)splits > capsp) splits = (int)capsp;
+  if (splits < 1) splits = 1;
+  const int kper = (ksteps + splits - 1) / splits * BG_KS;
+  splits = (K + kper - 1) / kper;
+  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr};
+  hipLaunchKernelGGL(k_bgemm, dim3(tiles * splits), dim3(256), 0, gc.s, g);
+  if (splits > 1) {
+    TG r{};
+    r.M = M; r.N = N; r.K = K; r.C = C; r.ldc = ldc; r.crow = crow; r.bias = bias; r.accumulate = accumulate;
+    r.splits = splits; r.kper = kper; r.part = gc.split;
+    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, gc.s, r);
+  }
+}
+static inline int rup64(int x) { return (x + 63) / 64 * 64; }
+static void pk_rows(hipStream_t st, const float* src, int64_t lds, const int* map, int rows, int cols, __bf16* dst, int Kp) {
+  const int64_t n = (int64_t)rows * (Kp / 8);
+  const int vec = lds % 4 == 0 && cols % 8 == 0 && ((uintptr_t)src & 15) == 0;
+  hipLaunchKernelGGL(k_pk_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, lds, map, rows, cols, dst, Kp,
+                     vec);
+}
+template <class S>
+static void pk_trans(hipStream_t st, const S* src, int64_t lds, int rows, int cols, __bf16* dst, int Kp) {
+  hipLaunchKernelGGL(k_pk_trans<S>, dim3((unsigned)(Kp / 64), (unsigned)((cols + 63) / 64)), dim3(256), 0, st, src, lds,
+                     rows, cols, dst, Kp);
+}
 
 // column sums: out[n] (+)= sum_m X[m ldx + n], deterministic: rows split into CS_CH fixed chunks
 // summed in order by k_colsum (one thread per (column, chunk)), the chunk sums added in chunk
@@ -655,11 +871,15 @@ __global__ __launch_bounds__(256) void k_tr_atb_img(int B, int TS, int G, const 
 }
 
 // copy a [rows][cols] matrix into pitch `pitch` (zero padding)
-__global__ void k_pad_rows(const float* __restrict__ src, int rows, int cols, int pitch, float* __restrict__ dst) {
+// (and, for the bf16 step's k_bgemm, the same matrix rounded to bf16: dstb, same pitch)
+__global__ void k_pad_rows(const float* __restrict__ src, int rows, int cols, int pitch, float* __restrict__ dst,
+                           __bf16* __restrict__ dstb = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)rows * pitch) return;
   const int r = (int)(i / pitch), c = (int)(i % pitch);
-  dst[i] = c < cols ? src[(int64_t)r * cols + c] : 0.f;
+  const float v = c < cols ? src[(int64_t)r * cols + c] : 0.f;
+  dst[i] = v;
+  if (dstb) dstb[i] = (__bf16)v;
 }
 
 // gather rows: dst[i] = src[rows[i]]
@@ -799,12 +1019,22 @@ __global__ void k_tanh_bwd(float* __restrict__ d, const float* __restrict__ y, i
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) d[i] = d[i] * (1.f - y[i] * y[i]);
 }
-__global__ void k_rowsum_pp(const float* __restrict__ X, int rows, float* __restrict__ out) {  // [rows][PP] -> [P]
-  const int j = threadIdx.x;
-  if (j >= P) return;
+// [rows][PP] -> [P], each column summed in row order; the rows' values are loaded by all 256
+// threads first (one thread looping over the rows waited for every load in turn: 30 us at 128 rows)
+constexpr int RS_ROWS = 256;  // rows staged per LDS pass
+__global__ __launch_bounds__(256) void k_rowsum_pp(const float* __restrict__ X, int rows, float* __restrict__ out) {
+  __shared__ float xs[RS_ROWS * P];
+  const int t = threadIdx.x;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += X[(int64_t)r * PP + j];
-  out[j] = s;
+  for (int r0 = 0; r0 < rows; r0 += RS_ROWS) {
+    const int n = rows - r0 < RS_ROWS ? rows - r0 : RS_ROWS;
+    __syncthreads();
+    for (int i = t; i < n * P; i += 256) xs[i] = X[(int64_t)(r0 + i / P) * PP + i % P];
+    __syncthreads();
+    if (t < P)
+      for (int r = 0; r < n; ++r) s += xs[r * P + t];
+  }
+  if (t < P) out[t] = s;
 }
 
 }  // namespace aa
@@ -812,7 +1042,7 @@ __global__ void k_rowsum_pp(const float* __restrict__ X, int rows, float* __rest
 // ---------------------------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------------------------
-constexpr size_t TR_SPLIT_FLOATS = (size_t)4 << 20;  // 16 MB split-K scratch
+constexpr size_t TR_SPLIT_FLOATS = (size_t)16 << 20;  // 64 MB split-K scratch (k_bgemm's splits of dU / dW_a)
 
 struct TrainWS {
   float *a_g, *V, *vg, *h0, *c0, *VWv, *X, *PRE, *G4, *GA, *Hs, *Cs, *SG, *S, *PG, *PS, *alpha, *beta, *ctx, *U;
@@ -821,6 +1051,9 @@ struct TrainWS {
   float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
   float *dA, *dag;  // d(features) pieces: through V [B*49][C] and through a_g [B][C]
   float *dz, *dwr;  // per-row dz and w_h-gradient terms of k_tr_atb_row, summed per image by k_tr_atb_img
+  // bf16 operands of the large GEMMs (AA_TRAIN_BF16, k_bgemm): U_p, W_m, dS (rows), W_m^T, dS^T, U_p^T,
+  // dV^T, the feature map as [C][B 49]
+  __bf16 *ub, *wmb, *dspb, *wmT, *dspT, *upT, *dvT, *ftT;
   int *trank, *tcount, *torder, *tsmall;
 };
 
@@ -886,6 +1119,17 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.tsmall = c.take<int>(R);
   w.dz = c.take<float>(R * PP_);
   w.dwr = c.take<float>(R * PP_);
+  {
+    const size_t Kv = ((size_t)d.vocab + 63) / 64 * 64, Kr = (R + 63) / 64 * 64, Kb = ((size_t)B * P_ + 63) / 64 * 64;
+    w.ub = c.take<__bf16>(R * H);
+    w.wmb = c.take<__bf16>((size_t)d.vocab * H);
+    w.dspb = c.take<__bf16>(R * Kv);
+    w.wmT = c.take<__bf16>(H * Kv);
+    w.dspT = c.take<__bf16>((size_t)d.vocab * Kr);
+    w.upT = c.take<__bf16>(H * Kr);
+    w.dvT = c.take<__bf16>(H * Kb);
+    w.ftT = c.take<__bf16>(Cc * Kb);
+  }
   *bytes = c.off;
   return w;
 }
@@ -970,7 +1214,13 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
   // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
   hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
-  tgemm(gc, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
+  if (gc.bf16 && H % 64 == 0) {
+    pk_rows(st, s.U, H, s.prow, N, H, s.ub, H);
+    pk_rows(st, w->mlp_w, H, nullptr, V, H, s.wmb, H);
+    bgemm(gc, N, V, H, s.ub, H, s.wmb, H, scores, V, w->mlp_b);
+  } else {
+    tgemm(gc, N, V, H, s.U, H, 0, w->mlp_w, H, 0, scores, V, 0, w->mlp_b, nullptr, 0, s.prow);
+  }
   return aa_launch_status();
 }
 
@@ -1057,11 +1307,22 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   const size_t RH = (size_t)R * H;
   // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)
   const int Vp = (V + 63) / 64 * 64;  // dscores re-pitched to whole 16-B rows for vector loads
-  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp, s.dsp);
+  const bool bg = gc.bf16 && H % 64 == 0;  // the large GEMMs on k_bgemm
+  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp, s.dsp,
+                     bg ? s.dspb : nullptr);
   AA_TRY(hipMemsetAsync(s.dU, 0, sizeof(float) * RH, st));
-  tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
   hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
-  tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
+  if (bg) {
+    const int Kv = Vp, Kn = rup64(N);                                     // dS as bf16 [N][Vp]: k_pad_rows
+    pk_trans(st, w->mlp_w, H, V, H, s.wmT, Kv);                            // W_m^T [H][Kv]
+    bgemm(gc, N, H, Kv, s.dspb, Kv, s.wmT, Kv, s.dU, H, nullptr, s.prow);  // dU[prow] = dS W_m
+    pk_trans(st, s.dspb, Vp, N, V, s.dspT, Kn);                            // dS^T [V][Kn]
+    pk_trans(st, s.Up, H, N, H, s.upT, Kn);                                // U_p^T [H][Kn]
+    bgemm(gc, V, H, Kn, s.dspT, Kn, s.upT, Kn, GRAD(mlp_w), H);            // dW_m = dS^T U_p
+  } else {
+    tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
+    tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
+  }
   colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
   // Atten backward (adaptive_attention.py:26-58)
   AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
@@ -1088,7 +1349,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   tgemm(gc, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
   tgemm(gc, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
   tgemm(gc, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
-  hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(64), 0, st, s.dwh, B, GRAD(att_affine_h_w));
+  hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(256), 0, st, s.dwh, B, GRAD(att_affine_h_w));
   // Sentinel backward (:79-83): h_{t-1} input = Hs[r - B] for r >= B, 0 for t = 0
   hipLaunchKernelGGL(k_tr_sent_bwd, dim3(nblk((int64_t)RH)), dim3(256), 0, st, s.dS, s.SG, s.Cs, s.dG, s.dC,
                      (int64_t)RH);
@@ -1134,7 +1395,14 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   tgemm(gc, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);
   colsum(st, s.dc_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_c0_b));
   hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, st, s.dV, s.V, (int64_t)B * P * H);
-  tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);                // dW_a = dV^T A
+  if (gc.bf16 && H % 64 == 0) {  // dW_a = dV^T A
+    const int Kb = rup64(B * P);
+    pk_trans(st, s.dV, H, B * P, H, s.dvT, Kb);
+    hipLaunchKernelGGL(k_pk_feats, dim3(nblk((int64_t)C * (Kb / 8))), dim3(256), 0, st, feats, B, C, s.ftT, Kb);
+    bgemm(gc, H, C, Kb, s.dvT, Kb, s.ftT, Kb, GRAD(enc_affine_a_w), C);
+  } else {
+    tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);              // dW_a = dV^T A
+  }
   colsum(st, s.dV, B * P, H, (int64_t)H, s.csum, GRAD(enc_affine_a_b));
   if (dfeats) {  // gradient into the trunk's output A (CNN fine-tuning, train.py:89)
     tgemm(gc, B * P, C, H, s.dV, H, 0, w->enc_affine_a_w, C, 1, s.dA, C);              // dA = dV W_a
