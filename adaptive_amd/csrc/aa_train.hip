@@ -352,6 +352,7 @@ struct BG {
   const float* bias;
   int accumulate, splits, kper;
   float* part;
+  int act;  // 0 none, 1 relu (after the bias)
 };
 __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BG_T * BG_LD];
@@ -436,7 +437,8 @@ __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
         if (g.splits > 1) {
           g.part[(int64_t)split * g.M * g.N + (int64_t)m * g.N + col] = acc[x][y][r];
         } else {
-          const float v = acc[x][y][r] + bv;
+          float v = acc[x][y][r] + bv;
+          if (g.act == 1) v = reluf_(v);
           float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
           *dst = g.accumulate ? *dst + v : v;
         }
@@ -484,6 +486,24 @@ __global__ __launch_bounds__(256) void k_pk_trans(const S* __restrict__ src, int
   }
 }
 
+// the NCHW feature map as the bf16 row matrix of the encoder GEMM V = relu(A W_a^T + b): dst[b 49 + p][c]
+// = feats[b][c][p]; a workgroup per (image, 64 channels) reads its 64 x 49 contiguous floats and writes
+// 49 rows of 128 B
+__global__ __launch_bounds__(256) void k_pk_featrows(const float* __restrict__ feats, int C, __bf16* __restrict__ dst) {
+  __shared__ float tile[64 * P];
+  const int b = blockIdx.y, c0 = blockIdx.x * 64, t = threadIdx.x;
+  const float* src = feats + ((int64_t)b * C + c0) * P;
+  for (int i = t; i < 64 * P; i += 256) tile[i] = src[i];  // [c][p]
+  __syncthreads();
+  for (int i = t; i < P * 8; i += 256) {  // row p, 8-channel piece j
+    const int p = i >> 3, j = i & 7;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)tile[(8 * j + e) * P + p];
+    *reinterpret_cast<bf16x8*>(dst + ((int64_t)b * P + p) * C + c0 + 8 * j) = v;
+  }
+}
+
 // the NCHW feature map as the K-contiguous operand of dW_a = dV^T A: dst[c][b 49 + p] = feats[b][c][p],
 // zero for rows >= B 49 up to Kp; 8 consecutive rows per thread (one 16-B store)
 __global__ void k_pk_feats(const float* __restrict__ feats, int B, int C, __bf16* __restrict__ dst, int Kp) {
@@ -508,7 +528,8 @@ __global__ void k_pk_feats(const float* __restrict__ feats, int B, int C, __bf16
 // C[M,N] (+)= A B^T (+ bias) on k_bgemm; K a multiple of 64.  Fewer than 512 tiles: split K to
 // ~1024 workgroups (bounded by the split scratch), partials reduced by k_tgemm_reduce in split order.
 static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb,
-                  float* C, int64_t ldc, const float* bias = nullptr, const int* crow = nullptr, int accumulate = 0) {
+                  float* C, int64_t ldc, const float* bias = nullptr, const int* crow = nullptr, int accumulate = 0,
+                  int act = 0) {
   if (M <= 0 || N <= 0 || K <= 0) return;
   const int tiles = ((M + BG_T - 1) / BG_T) * ((N + BG_T - 1) / BG_T), ksteps = K / BG_KS;
   int splits = tiles >= 512 ? 1 : (1024 + tiles - 1) / tiles;
@@ -518,12 +539,12 @@ static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64
   if (splits < 1) splits = 1;
   const int kper = (ksteps + splits - 1) / splits * BG_KS;
   splits = (K + kper - 1) / kper;
-  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr};
+  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr, act};
   hipLaunchKernelGGL(k_bgemm, dim3(tiles * splits), dim3(256), 0, gc.s, g);
   if (splits > 1) {
     TG r{};
     r.M = M; r.N = N; r.K = K; r.C = C; r.ldc = ldc; r.crow = crow; r.bias = bias; r.accumulate = accumulate;
-    r.splits = splits; r.kper = kper; r.part = gc.split;
+    r.splits = splits; r.kper = kper; r.part = gc.split; r.act = act;
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, gc.s, r);
   }
 }
@@ -1203,7 +1224,13 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
   // encoder tail (baseline_attention.py:46-60), reference weight layouts
   hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
-  {
+  if (gc.bf16 && H % 64 == 0 && C % 64 == 0) {
+    // bf16 step: V = relu(A W_a^T + b) on k_bgemm (the feature map and W_a packed to bf16 in buffers the
+    // backward pass reuses for its own operands)
+    hipLaunchKernelGGL(k_pk_featrows, dim3(C / 64, B), dim3(256), 0, st, feats, C, s.ftT);
+    pk_rows(st, w->enc_affine_a_w, C, nullptr, H, C, s.wmT, C);
+    bgemm(gc, B * P, H, C, s.ftT, C, s.wmT, C, s.V, H, w->enc_affine_a_b, nullptr, 0, 1);
+  } else {
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, st, feats, B, C, H, w->enc_affine_a_w,
                        w->enc_affine_a_b, s.V);
