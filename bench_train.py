@@ -136,7 +136,7 @@ def main():
     fl = train_flops(B, T, lengths)
     peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_FP32
     achieved = fl["total"] / (el / args.steps)
-    out["roofline"] = {"kernel": "whole step (k_tgemm GEMMs + elementwise + Adam)", "bound": "mfma",
+    out["roofline"] = {"kernel": "whole step (k_tgemm / k_bgemm GEMMs + elementwise + Adam)", "bound": "mfma",
                        "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
                        "traffic": None, "flops_per_step": fl["total"],
                        "note": "algorithmic GEMM FLOPs of forward + backward (bench_train.train_flops) over the "
