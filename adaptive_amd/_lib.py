@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 # AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
 LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libadaptive_amd.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_FUSED_LSTM = 4
@@ -73,6 +73,14 @@ class Model(Structure):
 TRACE_ENCODER_KERNELS = 5  # k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM
 
 
+class AdamTensor(Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", c_int64)]
+
+
+ADAM_MAX_TENSORS = 24
+
+
 class Trace(Structure):
     _fields_ = [("encoder_events", c_void_p), ("lstm_events", c_void_p), ("atten_events", c_void_p),
                 ("screen_events", c_void_p), ("rescore_events", c_void_p), ("gemm_events", c_void_p)]
@@ -118,6 +126,13 @@ SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int32, c_void_p, c_void_p]),
     "aa_vocab_logits": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_void_p]),
     "aa_vocab_logits_at": (c_int, [POINTER(Model), c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "aa_cross_entropy_workspace_bytes": (c_size_t, [c_int32]),
+    "aa_cross_entropy_forward": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                         c_void_p, c_size_t, c_void_p]),
+    "aa_cross_entropy_backward": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_int64, c_void_p]),
+    "aa_adam_step": (c_int, [POINTER(AdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double,
+                             c_double, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),
 }
 

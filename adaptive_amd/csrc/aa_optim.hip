@@ -1,0 +1,305 @@
+// aa_optim.hip — the two pieces of train.py's closure that sit around the teacher-forced
+// forward/backward (code_src/train.py:197-219): the CrossEntropyLoss on the packed scores and the
+// Adam step over every parameter.  Both are HBM-bound elementwise passes, so each is ONE launch
+// per call (Adam: every parameter tensor in one grid; cross entropy: one read of the scores
+// forward, one read + one write backward) instead of PyTorch's per-op kernel chains.
+//
+// Its own translation unit (linked into libadaptive_amd.so beside aa_kernels.hip).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "adaptive_amd.h"
+
+namespace aa_optim {
+
+// ---- Adam (torch.optim.Adam, amsgrad=False, maximize=False; model_factory.py:71 builds it) -------------
+// One workgroup = ADAM_CHUNK consecutive elements of one tensor.  The per-tensor table travels in
+// the kernel arguments (no upload, no allocation).
+constexpr int ADAM_THREADS = 256;
+constexpr int ADAM_VEC = 4;                                  // float4 per thread per round
+constexpr int ADAM_ROUNDS = 4;                               // rounds per workgroup
+constexpr int ADAM_CHUNK = ADAM_THREADS * ADAM_VEC * ADAM_ROUNDS;  // 4096 elements
+
+struct AdamArgs {
+  int n;                                  // tensors in this launch (<= AA_ADAM_MAX_TENSORS)
+  int aligned;                            // bit i: tensor i's four pointers are 16-byte aligned
+  int64_t blk0[AA_ADAM_MAX_TENSORS + 1];  // first workgroup of tensor i (prefix sum)
+  int64_t numel[AA_ADAM_MAX_TENSORS];
+  float* p[AA_ADAM_MAX_TENSORS];
+  const float* g[AA_ADAM_MAX_TENSORS];
+  float* m[AA_ADAM_MAX_TENSORS];
+  float* v[AA_ADAM_MAX_TENSORS];
+  float w1;         // 1 - beta1 (lerp weight)
+  float beta2;
+  float omb2;       // 1 - beta2
+  float bc2_sqrt;   // sqrt(1 - beta2^step)
+  float step_size;  // -lr / (1 - beta1^step)
+  float eps;
+  float wd;         // L2 weight decay (added to the gradient, as torch's Adam does)
+};
+
+// torch's foreach Adam, element by element, in its op order (optim/adam.py _multi_tensor_adam):
+// g' = g + wd p; m = lerp(m, g', 1-b1); v = v*b2; v = v + (1-b2)*(g'*g'); d = sqrt(v)/bc2s + eps;
+// p = p + step_size*(m/d).  lerp as ATen's (Lerp.h): |w| < 0.5 ? a + w(b-a) : b - (b-a)(1-w).
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
+  if (a.wd != 0.f) g = g + a.wd * p;
+  m = (fabsf(a.w1) < 0.5f) ? m + a.w1 * (g - m) : g - (g - m) * (1.f - a.w1);
+  v = v * a.beta2;
+  v = v + a.omb2 * (g * g);
+  const float d = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p + a.step_size * (m / d);
+}
+
+__global__ __launch_bounds__(ADAM_THREADS) void k_adam(AdamArgs a) {
+  const int64_t blk = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.n && blk >= a.blk0[t + 1]) ++t;  // <= 24 scalar compares
+  const int64_t base = (blk - a.blk0[t]) * ADAM_CHUNK;
+  const int64_t n = a.numel[t];
+  float* __restrict__ P = a.p[t];
+  const float* __restrict__ G = a.g[t];
+  float* __restrict__ M = a.m[t];
+  float* __restrict__ Vv = a.v[t];
+  if (((a.aligned >> t) & 1) && base + ADAM_CHUNK <= n) {
+    // full chunk, vector path: every load of the chunk issued before the arithmetic
+    float4 p4[ADAM_ROUNDS], g4[ADAM_ROUNDS], m4[ADAM_ROUNDS], v4[ADAM_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ADAM_ROUNDS; ++r) {
+      const int64_t i = base + ((int64_t)r * ADAM_THREADS + threadIdx.x) * ADAM_VEC;
+      p4[r] = *reinterpret_cast<const float4*>(P + i);
+      g4[r] = *reinterpret_cast<const float4*>(G + i);
+      m4[r] = *reinterpret_cast<const float4*>(M + i);
+      v4[r] = *reinterpret_cast<const float4*>(Vv + i);
+    }
+#pragma unroll
+    for (int r = 0; r < ADAM_ROUNDS; ++r) {
+      adam_elem(p4[r].x, g4[r].x, m4[r].x, v4[r].x, a);
+      adam_elem(p4[r].y, g4[r].y, m4[r].y, v4[r].y, a);
+      adam_elem(p4[r].z, g4[r].z, m4[r].z, v4[r].z, a);
+      adam_elem(p4[r].w, g4[r].w, m4[r].w, v4[r].w, a);
+      const int64_t i = base + ((int64_t)r * ADAM_THREADS + threadIdx.x) * ADAM_VEC;
+      *reinterpret_cast<float4*>(P + i) = p4[r];
+      *reinterpret_cast<float4*>(M + i) = m4[r];
+      *reinterpret_cast<float4*>(Vv + i) = v4[r];
+    }
+  } else {
+    // tail chunk or unaligned tensor: scalar, coalesced
+    const int64_t end = base + ADAM_CHUNK < n ? base + ADAM_CHUNK : n;
+    for (int64_t i = base + threadIdx.x; i < end; i += ADAM_THREADS) {
+      float p = P[i], m = M[i], v = Vv[i];
+      adam_elem(p, G[i], m, v, a);
+      P[i] = p;
+      M[i] = m;
+      Vv[i] = v;
+    }
+  }
+}
+
+// ---- cross entropy (nn.CrossEntropyLoss(), reduction mean; train.py:63,208) -------------------
+// Forward: one workgroup per row: lse_i = log sum_j exp(x_ij) (online max / sum, one read of the
+// row), loss_i = lse_i - x_i[t_i] (0 for ignored rows); then one workgroup sums loss_i in a fixed
+// order and divides by the number of counted rows.  Backward: dx_ij = (exp(x_ij - lse_i) - [j ==
+// t_i]) * dloss / count (0 for ignored rows): one read and one write of the scores.
+constexpr int CE_THREADS = 256;
+
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  if (m2 > m) {
+    s = s * expf(m - m2) + s2;
+    m = m2;
+  } else if (m2 != -INFINITY) {
+    s = s + s2 * expf(m2 - m);
+  }
+}
+
+__global__ __launch_bounds__(CE_THREADS) void k_ce_rows(const float* __restrict__ x, int64_t ldx, int V,
+                                                        const int64_t* __restrict__ tgt, int64_t ignore,
+                                                        float* __restrict__ lse_out, float* __restrict__ loss_out,
+                                                        int* __restrict__ valid_out) {
+  const int row = blockIdx.x;
+  const float* __restrict__ xr = x + (int64_t)row * ldx;
+  float m = -INFINITY, s = 0.f;
+  int j = threadIdx.x;
+  // eight independent loads in flight per lane, then the online update
+  for (; j + 7 * CE_THREADS < V; j += 8 * CE_THREADS) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xr[j + k * CE_THREADS];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lse_merge(m, s, v[k], 1.f);
+  }
+  for (; j < V; j += CE_THREADS) lse_merge(m, s, xr[j], 1.f);
+  // wave butterfly, then across the four waves through LDS (fixed order: deterministic)
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float m2 = __shfl_xor(m, off), s2 = __shfl_xor(s, off);
+    lse_merge(m, s, m2, s2);
+  }
+  __shared__ float sm[CE_THREADS / 64], ss[CE_THREADS / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[w] = m;
+    ss[w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int k = 1; k < CE_THREADS / 64; ++k) lse_merge(M, S, sm[k], ss[k]);
+    const float lse = M + logf(S);
+    const int64_t t = tgt[row];
+    float loss;
+    int valid = 1;
+    if (t == ignore) {
+      loss = 0.f;
+      valid = 0;
+    } else if (t < 0 || t >= V) {
+      loss = NAN;  // out-of-range class index: poison the loss (torch raises a device assert)
+    } else {
+      loss = lse - xr[t];
+    }
+    lse_out[row] = lse;
+    loss_out[row] = loss;
+    valid_out[row] = valid;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_ce_reduce(const float* __restrict__ loss_rows,
+                                                    const int* __restrict__ valid_rows, int N,
+                                                    float* __restrict__ loss, float* __restrict__ count) {
+  float s = 0.f;
+  int c = 0;
+  for (int i = threadIdx.x; i < N; i += 1024) {
+    s += loss_rows[i];
+    c += valid_rows[i];
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s += __shfl_xor(s, off);
+    c += __shfl_xor(c, off);
+  }
+  __shared__ float ws[16];
+  __shared__ int wc[16];
+  if ((threadIdx.x & 63) == 0) {
+    ws[threadIdx.x >> 6] = s;
+    wc[threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float S = 0.f;
+    int C = 0;
+    for (int k = 0; k < 16; ++k) {
+      S += ws[k];
+      C += wc[k];
+    }
+    count[0] = (float)C;
+    loss[0] = S / (float)C;
+  }
+}
+
+__global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* __restrict__ x, int64_t ldx, int V,
+                                                       const int64_t* __restrict__ tgt, int64_t ignore,
+                                                       const float* __restrict__ lse, const float* __restrict__ dloss,
+                                                       const float* __restrict__ count, float* __restrict__ dx,
+                                                       int64_t lddx) {
+  const int row = blockIdx.x;
+  const float* __restrict__ xr = x + (int64_t)row * ldx;
+  float* __restrict__ dr = dx + (int64_t)row * lddx;
+  const int64_t t = tgt[row];
+  const float scale = (t == ignore) ? 0.f : dloss[0] / count[0];
+  const float L = lse[row];
+  int j = threadIdx.x;
+  for (; j + 7 * CE_THREADS < V; j += 8 * CE_THREADS) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xr[j + k * CE_THREADS];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = j + k * CE_THREADS;
+      dr[c] = (expf(v[k] - L) - (c == t ? 1.f : 0.f)) * scale;
+    }
+  }
+  for (; j < V; j += CE_THREADS) dr[j] = (expf(xr[j] - L) - (j == t ? 1.f : 0.f)) * scale;
+}
+
+}  // namespace aa_optim
+
+using namespace aa_optim;
+
+extern "C" {
+
+int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, aa_stream_t stream) {
+  if (n < 0) return AA_ERR_SHAPE;
+  if (n > 0 && !tensors) return AA_ERR_NULL;
+  if (!(step >= 1.0)) return AA_ERR_SHAPE;
+  // step-invariant scalars exactly as torch computes them (Python doubles, cast to fp32 opmath)
+  const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
+  AdamArgs a;
+  a.w1 = (float)(1.0 - beta1);
+  a.beta2 = (float)beta2;
+  a.omb2 = (float)(1.0 - beta2);
+  a.bc2_sqrt = (float)sqrt(bc2);
+  a.step_size = (float)((lr / bc1) * -1.0);
+  a.eps = (float)eps;
+  a.wd = (float)weight_decay;
+  for (int i0 = 0; i0 < n; i0 += AA_ADAM_MAX_TENSORS) {  // one launch per AA_ADAM_MAX_TENSORS tensors
+    a.n = 0;
+    a.aligned = 0;
+    int64_t blocks = 0;
+    for (int i = i0; i < n && i < i0 + AA_ADAM_MAX_TENSORS; ++i) {
+      const aa_adam_tensor& T = tensors[i];
+      if (T.numel < 0) return AA_ERR_SHAPE;
+      if (T.numel == 0) continue;
+      if (!T.param || !T.grad || !T.exp_avg || !T.exp_avg_sq) return AA_ERR_NULL;
+      const int k = a.n++;
+      a.p[k] = (float*)T.param;
+      a.g[k] = (const float*)T.grad;
+      a.m[k] = (float*)T.exp_avg;
+      a.v[k] = (float*)T.exp_avg_sq;
+      a.numel[k] = T.numel;
+      const uintptr_t orp = (uintptr_t)T.param | (uintptr_t)T.grad | (uintptr_t)T.exp_avg | (uintptr_t)T.exp_avg_sq;
+      if ((orp & 15) == 0) a.aligned |= 1 << k;
+      a.blk0[k] = blocks;
+      blocks += (T.numel + ADAM_CHUNK - 1) / ADAM_CHUNK;
+    }
+    if (a.n == 0) continue;
+    a.blk0[a.n] = blocks;
+    if (blocks > 0x7fffffff) return AA_ERR_SHAPE;
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return AA_OK;
+}
+
+size_t aa_cross_entropy_workspace_bytes(int32_t N) {
+  return N <= 0 ? 0 : (size_t)N * 3 * sizeof(float);
+}
+
+int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, int64_t ldx, const int64_t* targets,
+                             int64_t ignore_index, float* loss, float* count, void* workspace,
+                             size_t workspace_bytes, aa_stream_t stream) {
+  if (N <= 0 || V <= 0 || ldx < V) return AA_ERR_SHAPE;
+  if (!logits || !targets || !loss || !count || !workspace) return AA_ERR_NULL;
+  if (workspace_bytes < aa_cross_entropy_workspace_bytes(N)) return AA_ERR_BUFFER;
+  float* lse = (float*)workspace;
+  float* rows = lse + N;
+  int* valid = (int*)(rows + N);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_ce_rows, dim3(N), dim3(CE_THREADS), 0, st, logits, ldx, V, targets, ignore_index, lse, rows,
+                     valid);
+  hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, st, rows, valid, N, loss, count);
+  return (int)hipGetLastError();
+}
+
+int aa_cross_entropy_backward(const float* logits, int32_t N, int32_t V, int64_t ldx, const int64_t* targets,
+                              int64_t ignore_index, const float* dloss, const float* count, const void* workspace,
+                              float* dlogits, int64_t lddx, aa_stream_t stream) {
+  if (N <= 0 || V <= 0 || ldx < V || lddx < V) return AA_ERR_SHAPE;
+  if (!logits || !targets || !dloss || !count || !workspace || !dlogits) return AA_ERR_NULL;
+  hipLaunchKernelGGL(k_ce_bwd, dim3(N), dim3(CE_THREADS), 0, (hipStream_t)stream, logits, ldx, V, targets,
+                     ignore_index, (const float*)workspace, dloss, count, dlogits, lddx);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

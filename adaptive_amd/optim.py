@@ -1,0 +1,156 @@
+"""The rest of train.py's closure around the teacher-forced step (code_src/train.py:63,197-219; models/model_factory.py:71):
+``CrossEntropyLoss`` on the packed scores and the ``Adam`` step, each one HIP launch chain through
+the C-ABI (``aa_cross_entropy_*``, ``aa_adam_step`` in adaptive_amd/csrc/aa_optim.hip) instead of
+PyTorch's per-op kernels (softmax + nll forward and backward; nine foreach passes for Adam).
+
+Drop-ins with the same constructor arguments, numerics (torch's op order, fp32) and state layout:
+
+    criterion = adaptive_amd.optim.CrossEntropyLoss()           # nn.CrossEntropyLoss()
+    optimizer = adaptive_amd.optim.Adam(params, lr=cf.lr)       # torch.optim.Adam(..., betas, weight_decay)
+
+``Adam.state_dict()`` has torch's keys (``step`` as a CPU float32 tensor, ``exp_avg``,
+``exp_avg_sq``), so a checkpoint moves between the two optimizers.  There is no CPU fallback: CPU
+tensors raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _require_hip(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"adaptive_amd.optim: {what} must be a GPU tensor (the HIP kernels have no CPU path)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"adaptive_amd.optim: {what} must be float32, got {t.dtype}")
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (model_factory.py:71: ``Adam(params, lr, betas, weight_decay)``) for fp32 GPU parameters:
+    amsgrad=False, maximize=False, L2 ``weight_decay`` added to the gradient.  Every parameter with a
+    gradient is updated by one ``aa_adam_step`` launch (per 24 tensors) in torch's foreach op order."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if amsgrad:
+            raise NotImplementedError("adaptive_amd.optim.Adam: amsgrad is not supported (train.py does not use it)")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                                      maximize=False, foreach=None, capturable=False, differentiable=False,
+                                      fused=None))
+        self._tables = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = _lib.load()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            by_step = {}  # tensors that share a step count go in one call
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
+                _require_hip(p, "parameter")
+                if not (p.is_contiguous() and p.grad.is_contiguous()):
+                    raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                by_step.setdefault((p.device, float(st["step"].item())), []).append(
+                    (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                     p.numel()))
+            for (dev, step), rows in by_step.items():
+                key = tuple(rows)
+                arr = self._tables.get(key)
+                if arr is None:  # cached per pointer set (the caching allocator hands back the same grads)
+                    arr = (_lib.AdamTensor * len(rows))(*[_lib.AdamTensor(*r) for r in rows])
+                    if len(self._tables) > 16:
+                        self._tables.clear()
+                    self._tables[key] = arr
+                with torch.cuda.device(dev):
+                    rc = lib.aa_adam_step(arr, len(rows), step, group["lr"], beta1, beta2, group["eps"],
+                                          group["weight_decay"], _lib.stream_handle())
+                _lib.check(rc, "adam_step")
+        return loss
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index):
+        lib = _lib.load()
+        N, V = logits.shape
+        x = logits if logits.stride(1) == 1 else logits.contiguous()
+        ws = torch.empty(lib.aa_cross_entropy_workspace_bytes(N), dtype=torch.uint8, device=x.device)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        count = torch.empty(1, dtype=torch.float32, device=x.device)
+        with torch.cuda.device(x.device):
+            rc = lib.aa_cross_entropy_forward(x.data_ptr(), N, V, x.stride(0), target.data_ptr(), ignore_index,
+                                              loss.data_ptr(), count.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              _lib.stream_handle())
+        _lib.check(rc, "cross_entropy_forward")
+        ctx.save_for_backward(x, target, ws, count)
+        ctx.ignore_index = ignore_index
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        lib = _lib.load()
+        x, target, ws, count = ctx.saved_tensors
+        N, V = x.shape
+        dloss = dloss.contiguous().float()
+        dx = torch.empty(N, V, dtype=torch.float32, device=x.device)
+        with torch.cuda.device(x.device):
+            rc = lib.aa_cross_entropy_backward(x.data_ptr(), N, V, x.stride(0), target.data_ptr(), ctx.ignore_index,
+                                               dloss.data_ptr(), count.data_ptr(), ws.data_ptr(), dx.data_ptr(),
+                                               dx.stride(0), _lib.stream_handle())
+        _lib.check(rc, "cross_entropy_backward")
+        return dx, None, None
+
+
+def cross_entropy(input: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """F.cross_entropy(input [N, C] fp32, target [N] class indices) with reduction 'mean' on the GPU:
+    one read of the scores forward, one read + one write backward (aa_cross_entropy_*)."""
+    _require_hip(input, "input")
+    if input.dim() != 2:
+        raise ValueError(f"adaptive_amd.optim.cross_entropy: input must be [N, C], got {tuple(input.shape)}")
+    if target.dim() != 1 or target.size(0) != input.size(0):
+        raise ValueError("adaptive_amd.optim.cross_entropy: target must be [N] class indices")
+    if target.dtype != torch.int64:
+        raise TypeError(f"adaptive_amd.optim.cross_entropy: target must be int64, got {target.dtype}")
+    target = target.to(input.device).contiguous()
+    if input.size(0) == 0:  # torch: mean over no rows is NaN
+        return input.sum() * float("nan")
+    return _CrossEntropy.apply(input, target, int(ignore_index))
+
+
+class CrossEntropyLoss(torch.nn.Module):
+    """nn.CrossEntropyLoss() (train.py:63) for [N, C] fp32 GPU scores and int64 targets; reduction
+    'mean' with torch's ``ignore_index`` (weights and label smoothing are not used by the reference)."""
+
+    def __init__(self, ignore_index: int = -100, reduction: str = "mean"):
+        super().__init__()
+        if reduction != "mean":
+            raise NotImplementedError("adaptive_amd.optim.CrossEntropyLoss: only reduction='mean' (train.py:63)")
+        self.ignore_index = ignore_index
+
+    def forward(self, input, target):
+        return cross_entropy(input, target, self.ignore_index)
+
+
+__all__ = ["Adam", "CrossEntropyLoss", "cross_entropy"]

@@ -5,6 +5,10 @@ of Encoder2Decoder at B=128, captions of T=18 steps (+ <start>), on 1 MI355X:
     zero_grad -> forward (HIP, teacher-forced) -> CrossEntropyLoss on the packed scores
     -> backward (HIP) -> clip_grad_norm_(LSTM, 5) -> Adam step          (train.py:197-219)
 
+The loss and the optimizer are adaptive_amd.optim's HIP CrossEntropyLoss and Adam by default (one
+launch chain each, same numerics as torch's; tests/test_gpu_optim.py); --loss torch / --opt torch
+run PyTorch's nn.CrossEntropyLoss / torch.optim.Adam instead.
+
 Synthetic data: post-trunk features [B,2048,7,7] U[0,1), random captions with lengths 18 .. 9
 sorted descending, random-init weights of the reference architecture.  bf16 GEMMs (fp32 accumulate,
 fp32 master weights and elementwise work; BASELINE config 5) by default, --dtype fp32 for fp32 GEMMs.  Prints ONE
@@ -22,7 +26,6 @@ import time
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 from torch.nn.utils.rnn import pack_padded_sequence
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -61,12 +64,12 @@ def train_flops(B, T, lengths, E=256, H=512, V=10123, C=2048, P=49):
     return {"total": fwd + bwd + ctx, "forward": fwd + ctx, "backward": bwd, "gemms": g}
 
 
-def step(model, opt, feats, caps, lengths):
+def step(model, opt, crit, feats, caps, lengths):
+    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]  # train.py:102, per batch
     model.zero_grad()
     opt.zero_grad()
     packed = model(feats, caps, lengths)
-    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]
-    loss = F.cross_entropy(packed[0], targets)
+    loss = crit(packed[0], targets)
     loss.backward()
     torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
     opt.step()
@@ -107,6 +110,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
                     help="GEMM operand type: bf16 (AA_TRAIN_BF16, BASELINE config 5) or fp32")
+    ap.add_argument("--loss", choices=("hip", "torch"), default="hip",
+                    help="CrossEntropyLoss: adaptive_amd.optim (HIP) or torch.nn")
+    ap.add_argument("--opt", choices=("hip", "torch"), default="hip",
+                    help="Adam: adaptive_amd.optim (HIP, one launch) or torch.optim (foreach)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, T = args.batch, args.T
@@ -115,13 +122,15 @@ def main():
     model.train_bf16 = args.dtype == "bf16"
     feats = synthetic_features(B, dev, seed=0)
     caps = torch.from_numpy(caps_np).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    from adaptive_amd import optim as aa_optim
+    opt = (aa_optim.Adam if args.opt == "hip" else torch.optim.Adam)(model.parameters(), lr=1e-4)
+    crit = aa_optim.CrossEntropyLoss() if args.loss == "hip" else torch.nn.CrossEntropyLoss()
     for _ in range(args.warmup):
-        step(model, opt, feats, caps, lengths)
+        step(model, opt, crit, feats, caps, lengths)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step(model, opt, feats, caps, lengths)
+        loss = step(model, opt, crit, feats, caps, lengths)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out = {"metric": "training steps/s (teacher-forced fwd+bwd+Adam, B=128, T=18)", "value": args.steps / el,
@@ -131,7 +140,10 @@ def main():
            "config": {"workload": f"Encoder2Decoder.forward + CE + backward + clip + Adam, B={B}, T={T}",
                       "batch": B, "T": T, "packed_rows": int(sum(lengths)),
                       "gemm": "bf16 operands, fp32 accumulate (v_mfma_f32_32x32x16_bf16), fp32 master weights / Adam"
-                      if args.dtype == "bf16" else "fp32 (v_mfma_f32_32x32x2f32)"},
+                      if args.dtype == "bf16" else "fp32 (v_mfma_f32_32x32x2f32)",
+                      "loss": "adaptive_amd.optim.CrossEntropyLoss (HIP)" if args.loss == "hip" else "torch.nn.CrossEntropyLoss",
+                      "optimizer": "adaptive_amd.optim.Adam (HIP, one launch)" if args.opt == "hip"
+                      else "torch.optim.Adam (foreach)"},
            "final_loss": float(loss.item()), "cpu_baseline": None}
     fl = train_flops(B, T, lengths)
     peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_FP32

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 13
+#define AA_ABI_VERSION 14
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -334,6 +334,43 @@ AA_API int aa_vocab_logits(const aa_model* m, int32_t B, const float* u, float* 
  * (entries outside [0, vocab) give 0); out [B,n].  Used to rescore candidate tokens. */
 AA_API int aa_vocab_logits_at(const aa_model* m, int32_t B, const float* u, const int32_t* cols,
                               int32_t n, float* out, aa_stream_t stream);
+
+/* ---- the rest of train.py's closure: CrossEntropyLoss and Adam ------------
+ * aa_cross_entropy_forward: nn.CrossEntropyLoss()(logits, targets) (train.py:63,208; reduction
+ * 'mean', ignore_index as torch's, default -100): logits [N][ldx] fp32 (V used columns), targets [N]
+ * int64; writes loss[0] = mean over counted rows of (logsumexp(x_i) - x_i[t_i]) and count[0] = the
+ * number of counted rows (as float), and keeps the per-row log-sum-exp in the workspace
+ * (aa_cross_entropy_workspace_bytes(N)) for the backward.  A target outside [0, V) that is not
+ * ignore_index makes the loss NaN (torch raises a device-side assert).  Deterministic (fixed-order
+ * reductions).  aa_cross_entropy_backward: dlogits = (softmax(x_i) - onehot(t_i)) * dloss[0] /
+ * count[0] (0 for ignored rows), dloss a DEVICE scalar (the incoming gradient of the loss), with the
+ * forward's workspace; dlogits may alias logits only if lddx == ldx. */
+AA_API size_t aa_cross_entropy_workspace_bytes(int32_t N);
+AA_API int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, int64_t ldx,
+                                    const int64_t* targets, int64_t ignore_index, float* loss,
+                                    float* count, void* workspace, size_t workspace_bytes,
+                                    aa_stream_t stream);
+AA_API int aa_cross_entropy_backward(const float* logits, int32_t N, int32_t V, int64_t ldx,
+                                     const int64_t* targets, int64_t ignore_index, const float* dloss,
+                                     const float* count, const void* workspace, float* dlogits,
+                                     int64_t lddx, aa_stream_t stream);
+
+/* aa_adam_step: one torch.optim.Adam step (model_factory.py:71: Adam(params, lr, betas, weight_decay); amsgrad=False,
+ * maximize=False, L2 weight_decay added to the gradient) over n fp32 tensors, every tensor in one
+ * launch per AA_ADAM_MAX_TENSORS.  step = the step count AFTER this step's increment (1 on the first
+ * step).  Element-wise in torch's foreach op order (optim/adam.py _multi_tensor_adam):
+ * m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g; p += (-lr/(1-b1^step)) * m / (sqrt(v)/sqrt(1-b2^step) + eps).
+ * Tensors with numel 0 are skipped; the four pointers of a tensor must not overlap each other. */
+#define AA_ADAM_MAX_TENSORS 24
+typedef struct aa_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} aa_adam_tensor;
+AA_API int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double lr, double beta1,
+                        double beta2, double eps, double weight_decay, aa_stream_t stream);
 
 /* Counter-based synthetic data (same bits as adaptive_amd/synth.py):
  * dst[i] = fp32(lo + (hi - lo) * u(key, start + i)), u = (splitmix64(key + (start+i+1)*GOLDEN) >> 40) / 2^24.

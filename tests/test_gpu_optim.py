@@ -1,0 +1,132 @@
+"""GPU: adaptive_amd.optim against PyTorch's own ops on the same inputs -- the HIP cross entropy
+(aa_cross_entropy_*) against F.cross_entropy (train.py:63,208), the HIP Adam (aa_adam_step)
+against torch.optim.Adam (model_factory.py:71), and train.py's closure (train.py:197-219) with both
+against the closure with torch's.  Tolerances: fp32, written per assertion (the two sides round
+exp/log and the reductions in different orders; Adam is in torch's op order)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _scores(dev, N, V, seed=0, scale=4.0):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(N, V, generator=g) * scale).to(dev)
+    t = torch.randint(0, V, (N,), generator=g).to(dev)
+    return x, t
+
+
+@pytest.mark.parametrize("N,V,ignore", [(1741, 10123, False), (1741, 10123, True), (5, 3, False), (300, 1, False),
+                                        (64, 40000, True)])
+def test_cross_entropy_matches_torch(gpu_device, N, V, ignore):
+    from adaptive_amd.optim import cross_entropy
+    x, t = _scores(gpu_device, N, V)
+    if ignore:
+        t[::7] = -100
+    xa = x.clone().requires_grad_()
+    xr = x.clone().requires_grad_()
+    la = cross_entropy(xa, t)
+    lr = F.cross_entropy(xr, t)
+    (la * 1.7).backward()
+    (lr * 1.7).backward()
+    assert abs(la.item() - lr.item()) <= 2e-6 * abs(lr.item()) + 1e-7, (la.item(), lr.item())
+    err = (xa.grad - xr.grad).abs().max().item()
+    assert err <= 1e-5 * xr.grad.abs().max().item(), err
+    assert torch.all(xa.grad[t == -100] == 0)
+
+
+def test_cross_entropy_strided_input_deterministic_and_poisoned_target(gpu_device):
+    from adaptive_amd.optim import CrossEntropyLoss
+    wide, t = _scores(gpu_device, 257, 10200, seed=3)
+    x = wide[:, :10123]  # row pitch 10200 > V: read in place, no copy
+    crit = CrossEntropyLoss()
+    l1, l2 = crit(x, t), crit(x, t)
+    assert l1.item() == l2.item()  # fixed-order reductions
+    assert abs(l1.item() - F.cross_entropy(x, t).item()) <= 2e-6 * abs(l1.item())
+    bad = t.clone()
+    bad[5] = 10123
+    assert torch.isnan(crit(x, bad)).item()
+
+
+def _adam_pair(dev, wd, betas, n_extra=0):
+    torch.manual_seed(0)
+    shapes = [(10123, 512), (10123,), (2048, 768), (2048,), (49, 512), (7,), (1000, 3)] + [(33,)] * n_extra
+    base = [torch.randn(s, device=dev) for s in shapes]
+    buf = torch.randn(4097, device=dev)
+    # the last parameter sits 4 bytes into its buffer: the kernel's unaligned (scalar) path
+    pa = [b.clone().requires_grad_() for b in base] + [buf[1:].detach().requires_grad_()]
+    pr = [p.detach().clone().requires_grad_() for p in pa]
+    return pa, pr
+
+
+@pytest.mark.parametrize("wd,betas,n_extra", [(0.0, (0.9, 0.999), 0), (1e-4, (0.8, 0.999), 0), (0.0, (0.9, 0.99), 30)])
+def test_adam_matches_torch(gpu_device, wd, betas, n_extra):
+    from adaptive_amd.optim import Adam
+    pa, pr = _adam_pair(gpu_device, wd, betas, n_extra)
+    assert pa[-1].data_ptr() % 16 != 0
+    oa = Adam(pa, lr=1e-3, betas=betas, weight_decay=wd)
+    orf = torch.optim.Adam(pr, lr=1e-3, betas=betas, weight_decay=wd)
+    g = torch.Generator(device=gpu_device).manual_seed(1)
+    worst = 0.0
+    for step in range(4):
+        for i, (a, r) in enumerate(zip(pa, pr)):
+            gr = torch.randn(a.shape, device=gpu_device, generator=g) * 10.0 ** -(i % 3)
+            a.grad, r.grad = gr.clone(), gr.clone()
+        if step == 2:
+            pa[1].grad = pr[1].grad = None  # a parameter without a gradient is left alone
+        oa.step()
+        orf.step()
+        for a, r in zip(pa, pr):
+            worst = max(worst, (a - r).abs().max().item())
+            sa, sr = oa.state[a], orf.state[r]
+            assert float(sa["step"]) == float(sr["step"])
+            assert torch.allclose(sa["exp_avg"], sr["exp_avg"], rtol=1e-6, atol=1e-9)
+            assert torch.allclose(sa["exp_avg_sq"], sr["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+    assert worst <= 2e-7, worst  # a few ulp of parameters ~1 after four lr=1e-3 steps
+    # the state dict moves to torch's Adam and back
+    orf2 = torch.optim.Adam(pr, lr=1e-3, betas=betas, weight_decay=wd)
+    orf2.load_state_dict(oa.state_dict())
+    oa2 = Adam(pa, lr=1e-3, betas=betas, weight_decay=wd)
+    oa2.load_state_dict(orf.state_dict())
+    assert float(oa2.state[pa[0]]["step"]) == 4.0
+
+
+def test_train_closure_with_hip_loss_and_adam(gpu_device):
+    """train.py:197-219 closure, three steps at B=16, T=10 (bf16 GEMMs): HIP CrossEntropyLoss + HIP
+    Adam against torch's on a second copy of the same model: the losses and parameters agree to
+    fp32 rounding (the forward/backward kernels are the same, so only the loss and the update differ)."""
+    from torch.nn.utils.rnn import pack_padded_sequence
+    from adaptive_amd import Config, Encoder2Decoder
+    from adaptive_amd.adaptive_attention import synthetic_features
+    from adaptive_amd.optim import Adam, CrossEntropyLoss
+    B, T = 16, 10
+    rng = np.random.default_rng(0)
+    lengths = sorted(rng.integers(T // 2, T + 1, size=B).tolist(), reverse=True)
+    lengths[0] = T
+    caps = torch.from_numpy(rng.integers(2, 10123, size=(B, T + 1))).to(gpu_device)
+    caps[:, 0] = 1
+    feats = synthetic_features(B, gpu_device, seed=0)
+    targets = pack_padded_sequence(caps[:, 1:], lengths, batch_first=True)[0]
+    runs = []
+    for hip in (True, False):
+        model = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
+        model.train_bf16 = True
+        opt = (Adam if hip else torch.optim.Adam)(model.parameters(), lr=1e-3)
+        crit = CrossEntropyLoss() if hip else torch.nn.CrossEntropyLoss()
+        losses = []
+        for _ in range(3):
+            model.zero_grad()
+            opt.zero_grad()
+            loss = crit(model(feats, caps, lengths)[0], targets)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+            opt.step()
+            losses.append(loss.item())
+        runs.append((losses, {k: v.detach().clone() for k, v in model.state_dict().items()}))
+    (la, sa), (lr, sr) = runs
+    assert np.allclose(la, lr, rtol=2e-6, atol=0), (la, lr)
+    for k in sr:
+        err = (sa[k] - sr[k]).abs().max().item()
+        assert err <= 2e-5 * max(1.0, sr[k].abs().max().item()), (k, err)
