@@ -899,7 +899,7 @@ __global__ void k_pad_rows(const float* __restrict__ src, int rows, int cols, in
   if (i >= (int64_t)rows * pitch) return;
   const int r = (int)(i / pitch), c = (int)(i % pitch);
   const float v = c < cols ? src[(int64_t)r * cols + c] : 0.f;
-  dst[i] = v;
+  if (dst) dst[i] = v;
   if (dstb) dstb[i] = (__bf16)v;
 }
 
@@ -1335,8 +1335,10 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)
   const int Vp = (V + 63) / 64 * 64;  // dscores re-pitched to whole 16-B rows for vector loads
   const bool bg = gc.bf16 && H % 64 == 0;  // the large GEMMs on k_bgemm
-  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp, s.dsp,
-                     bg ? s.dspb : nullptr);
+  // bf16 steps need dS only as bf16 (the GEMMs) and fp32 for db_m, which colsum reads from dscores
+  // itself (same sums, same order): no fp32 re-pitched copy
+  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp,
+                     bg ? nullptr : s.dsp, bg ? s.dspb : nullptr);
   AA_TRY(hipMemsetAsync(s.dU, 0, sizeof(float) * RH, st));
   hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
   if (bg) {
@@ -1350,7 +1352,8 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
     tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
   }
-  colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
+  if (bg) colsum(st, dscores, N, V, (int64_t)V, s.csum, GRAD(mlp_b));
+  else colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
   // Atten backward (adaptive_attention.py:26-58)
   AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
   AA_TRY(hipMemsetAsync(s.dPG, 0, sizeof(float) * (size_t)R * PP, st));
