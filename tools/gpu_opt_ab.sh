@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/opt1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_optim.py -v --timeout 120 --timeout-method thread -o cache_dir=/tmp/pc > gpurun_out/opt1/pytest.log 2>&1; rc=$?; tail -15 gpurun_out/opt1/pytest.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -o cache_dir=/tmp/pc > gpurun_out/opt1/pytest.log 2>&1; rc=$?; grep -E "FAIL|ERROR|passed|failed" gpurun_out/opt1/pytest.log | tail -25
 [ $rc -le 1 ] || exit $rc
 for v in "--opt torch --loss torch" "" "--opt torch --loss torch" ""; do
   timeout -k 10 200 python bench_train.py --no-cpu-baseline --steps 40 $v > gpurun_out/opt1/bt.json || exit $?
