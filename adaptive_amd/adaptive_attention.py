@@ -662,9 +662,19 @@ class Encoder2Decoder(nn.Module):
             raise ValueError("lengths exceed the caption width")
         dev = images.device
         caps = captions.to(device=dev, dtype=torch.int64).contiguous()
-        len_dev = torch.tensor(lengths, dtype=torch.int32, device=dev)
+        # the lengths on the device, cached per distinct lengths list: a fresh torch.tensor(...,
+        # device=dev) is a pageable host->device copy, which HIP may stage synchronously (the host
+        # then waits before it can queue the rest of the step)
+        cache = self.__dict__.setdefault("_len_dev_cache", {})
+        key = (dev, tuple(lengths))
+        len_dev = cache.get(key)
+        if len_dev is None:
+            if len(cache) > 64:
+                cache.clear()
+            len_dev = cache[key] = torch.tensor(lengths, dtype=torch.int32, device=dev)
         batch_sizes = torch.tensor([sum(1 for n in lengths if n > t) for t in range(T)], dtype=torch.int64)
-        params = [dict(self.named_parameters())[k] for _, k in _lib.WEIGHT_FIELDS]
+        named = dict(self.named_parameters())
+        params = [named[k] for _, k in _lib.WEIGHT_FIELDS]
         data = _TeacherForced.apply(self, images, caps, len_dev, sum(lengths), T, *params)
         return PackedSequence(data, batch_sizes)
 
