@@ -14,7 +14,7 @@ sorted descending, random-init weights of the reference architecture.  bf16 GEMM
 fp32 master weights and elementwise work; BASELINE config 5) by default, --dtype fp32 for fp32 GEMMs.  Prints ONE
 JSON line (steps/s; ms/step; the CPU oracle's autograd step timed on this host beside it).
 
-    python bench_train.py [--steps 20] [--warmup 3] [--batch 128] [--T 18] [--no-cpu-baseline]
+    python bench_train.py [--steps 50] [--warmup 3] [--batch 128] [--T 18] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -102,7 +102,7 @@ def cpu_baseline(caps, lengths, B, budget_s):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--T", type=int, default=18)
