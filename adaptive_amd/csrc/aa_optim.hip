@@ -97,8 +97,8 @@ __global__ __launch_bounds__(ADAM_THREADS) void k_adam(AdamArgs a) {
 }
 
 // ---- cross entropy (nn.CrossEntropyLoss(), reduction mean; train.py:63,208) -------------------
-// Forward: one workgroup per row: lse_i = log sum_j exp(x_ij) (online max / sum, one read of the
-// row), loss_i = lse_i - x_i[t_i] (0 for ignored rows); then one workgroup sums loss_i in a fixed
+// Forward: one workgroup per row: lse_i = log sum_j exp(x_ij) (one read of the row: in registers for
+// rows up to 12288 scores, an online max / sum beyond), loss_i = lse_i - x_i[t_i] (0 for ignored rows); then one workgroup sums loss_i in a fixed
 // order and divides by the number of counted rows.  Backward: dx_ij = (exp(x_ij - lse_i) - [j ==
 // t_i]) * dloss / count (0 for ignored rows): one read and one write of the scores.
 constexpr int CE_THREADS = 256;
@@ -154,6 +154,68 @@ __global__ __launch_bounds__(CE_THREADS) void k_ce_rows(const float* __restrict_
       valid = 0;
     } else if (t < 0 || t >= V) {
       loss = NAN;  // out-of-range class index: poison the loss (torch raises a device assert)
+    } else {
+      loss = lse - xr[t];
+    }
+    lse_out[row] = lse;
+    loss_out[row] = loss;
+    valid_out[row] = valid;
+  }
+}
+
+// Rows of up to CE_THREADS * CE_NPT scores: the row is held in registers (every load of the row in
+// flight at once), then max and sum exp(x - max) as two fixed-order block reductions: one exp per
+// score and no data-dependent branch (the online loop above pays a compare and branch per score).
+constexpr int CE_NPT = 48;
+
+__device__ __forceinline__ float block_reduce(float x, bool is_max, float* red) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float o = __shfl_xor(x, off);
+    x = is_max ? fmaxf(x, o) : x + o;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = x;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int k = 1; k < CE_THREADS / 64; ++k) r = is_max ? fmaxf(r, red[k]) : r + red[k];
+  __syncthreads();  // red is reused by the next reduction
+  return r;
+}
+
+__global__ __launch_bounds__(CE_THREADS) void k_ce_rows_reg(const float* __restrict__ x, int64_t ldx, int V,
+                                                            const int64_t* __restrict__ tgt, int64_t ignore,
+                                                            float* __restrict__ lse_out, float* __restrict__ loss_out,
+                                                            int* __restrict__ valid_out) {
+  const int row = blockIdx.x;
+  const float* __restrict__ xr = x + (int64_t)row * ldx;
+  __shared__ float red[CE_THREADS / 64];
+  float v[CE_NPT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < CE_NPT; ++k) {
+    const int j = threadIdx.x + k * CE_THREADS;
+    v[k] = j < V ? xr[j] : -INFINITY;
+  }
+#pragma unroll
+  for (int k = 0; k < CE_NPT; ++k) m = fmaxf(m, v[k]);
+  const float M = block_reduce(m, true, red);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CE_NPT; ++k)
+    if (threadIdx.x + k * CE_THREADS < V) s += expf(v[k] - M);
+  const float S = block_reduce(s, false, red);
+  if (threadIdx.x == 0) {
+    const float lse = M + logf(S);
+    const int64_t t = tgt[row];
+    float loss;
+    int valid = 1;
+    if (t == ignore) {
+      loss = 0.f;
+      valid = 0;
+    } else if (t < 0 || t >= V) {
+      loss = NAN;
     } else {
       loss = lse - xr[t];
     }
@@ -286,8 +348,12 @@ int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, int64_t 
   float* rows = lse + N;
   int* valid = (int*)(rows + N);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_ce_rows, dim3(N), dim3(CE_THREADS), 0, st, logits, ldx, V, targets, ignore_index, lse, rows,
-                     valid);
+  if (V <= CE_THREADS * CE_NPT)
+    hipLaunchKernelGGL(k_ce_rows_reg, dim3(N), dim3(CE_THREADS), 0, st, logits, ldx, V, targets, ignore_index, lse,
+                       rows, valid);
+  else
+    hipLaunchKernelGGL(k_ce_rows, dim3(N), dim3(CE_THREADS), 0, st, logits, ldx, V, targets, ignore_index, lse, rows,
+                       valid);
   hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, st, rows, valid, N, loss, count);
   return (int)hipGetLastError();
 }
