@@ -8,11 +8,12 @@ tag=${1:-run}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
+exec 3>&1  # step reports go to the script's stdout even when a step's output is redirected
 step() {  # name, then the command; stop unless it passed (0) or only had test failures (1)
   local name=$1; shift
   "$@"; local rc=$?
-  echo "[$name] exit $rc"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[$name] crashed or timed out: stopping"; exit $rc; fi
+  echo "[$name] exit $rc" >&3
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[$name] crashed or timed out: stopping" >&3; exit $rc; fi
 }
 step tests timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -o cache_dir=/tmp/pc > $out/pytest_gpu.log 2>&1
 grep -E "FAILED|ERROR|passed|failed" $out/pytest_gpu.log | tail -12
