@@ -1339,7 +1339,9 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   // itself (same sums, same order): no fp32 re-pitched copy
   hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp,
                      bg ? nullptr : s.dsp, bg ? s.dspb : nullptr);
-  AA_TRY(hipMemsetAsync(s.dU, 0, sizeof(float) * RH, st));
+  // dU, dS, dPG, dPS are carved back to back: one clear for the four (nothing below touches dS / dPG
+  // / dPS before the attention backward accumulates into them)
+  AA_TRY(hipMemsetAsync(s.dU, 0, (size_t)((char*)(s.dPS + (size_t)R * PP) - (char*)s.dU), st));
   hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
   if (bg) {
     const int Kv = Vp, Kn = rup64(N);                                     // dS as bf16 [N][Vp]: k_pad_rows
@@ -1355,9 +1357,6 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   if (bg) colsum(st, dscores, N, V, (int64_t)V, s.csum, GRAD(mlp_b));
   else colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
   // Atten backward (adaptive_attention.py:26-58)
-  AA_TRY(hipMemsetAsync(s.dS, 0, sizeof(float) * RH, st));
-  AA_TRY(hipMemsetAsync(s.dPG, 0, sizeof(float) * (size_t)R * PP, st));
-  AA_TRY(hipMemsetAsync(s.dPS, 0, sizeof(float) * (size_t)R * PP, st));
   int G, TS;
   atb_groups(B, T, &G, &TS);
 #define AA_ATB(HPT_)                                                                                          \
@@ -1388,8 +1387,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   tgemm(gc, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
   tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
   // LSTM backward through time (baseline_attention.py:167-178)
-  AA_TRY(hipMemsetAsync(s.dh_rec, 0, sizeof(float) * (size_t)B * H, st));
-  AA_TRY(hipMemsetAsync(s.dc_rec, 0, sizeof(float) * (size_t)B * H, st));
+  AA_TRY(hipMemsetAsync(s.dh_rec, 0, (size_t)((char*)(s.dc_rec + (size_t)B * H) - (char*)s.dh_rec), st));  // adjacent
   int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
   for (int t = T - 1; t >= 0; --t) {
     const size_t o = (size_t)t * B * H;

@@ -1,6 +1,6 @@
 set -u
 mkdir -p gpurun_out/ce2
-timeout -k 10 300 python -u -m pytest tests/test_gpu_optim.py tests/test_gpu_train.py -v --timeout 200 --timeout-method thread -o cache_dir=/tmp/pc > gpurun_out/ce2/pytest.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_optim.py tests/test_gpu_train.py tests/test_gpu_configs.py -v --timeout 200 --timeout-method thread -o cache_dir=/tmp/pc > gpurun_out/ce2/pytest.log 2>&1; rc=$?
 grep -E "FAILED|passed|failed" gpurun_out/ce2/pytest.log | tail -8
 [ $rc -le 1 ] || exit $rc
 export TMPDIR=/tmp
