@@ -6,11 +6,11 @@ ctypes and wrapped in a drop-in ``Encoder2Decoder`` module.
 """
 from .synth import Dims, make_features, make_weights  # noqa: F401
 
-__all__ = ["Dims", "make_features", "make_weights", "Encoder2Decoder", "Config"]
+__all__ = ["Dims", "make_features", "make_weights", "Encoder2Decoder", "Config", "DecodePlan"]
 
 
 def __getattr__(name):  # lazy: importing the package must not require torch/HIP
-    if name in ("Encoder2Decoder", "Config", "synthetic_features"):
+    if name in ("Encoder2Decoder", "Config", "synthetic_features", "DecodePlan"):
         from . import adaptive_attention
         return getattr(adaptive_attention, name)
     raise AttributeError(name)

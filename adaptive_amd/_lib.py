@@ -17,18 +17,12 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 # AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
 LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libadaptive_amd.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
-DECODE_FUSED_LSTM = 4
-DECODE_SCREEN64 = 8
-DECODE_ENC_V3 = 16
-DECODE_LISTS = 32
 DECODE_ONE_STREAM = 512
-BEAM_TILE128 = 64
 BEAM_FAST = 256
 TRAIN_BF16 = 128
-MAX_LANES = 8
 MAX_BEAM = 8
 
 
@@ -104,11 +98,8 @@ SIGNATURES = {
                                  c_size_t, POINTER(Trace), c_int32, c_void_p]),
     "aa_greedy_decode_aux": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, POINTER(Trace), c_int32, c_void_p, c_void_p]),
-    "aa_greedy_decode_lanes": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_size_t, POINTER(Trace), c_int32, c_void_p, POINTER(c_void_p),
-                                       c_int32]),
     "aa_decode_plan_create": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
-                                      c_void_p, c_size_t, c_int32, c_int32, POINTER(c_void_p)]),
+                                      c_void_p, c_size_t, c_int32, POINTER(c_void_p)]),
     "aa_decode_plan_launch": (c_int, [c_void_p, c_void_p]),
     "aa_decode_plan_destroy": (c_int, [c_void_p]),
     "aa_train_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
@@ -130,10 +121,11 @@ SIGNATURES = {
     "aa_cross_entropy_forward": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                          c_void_p, c_size_t, c_void_p]),
     "aa_cross_entropy_backward": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
-                                          c_void_p, c_void_p, c_int64, c_void_p]),
+                                          c_void_p, c_size_t, c_void_p, c_int64, c_void_p]),
     "aa_adam_step": (c_int, [POINTER(AdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double,
                              c_double, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),
+    "aa_read_probe": (c_int, [c_void_p, c_size_t, c_void_p, c_int32, c_void_p]),
 }
 
 _lib = None

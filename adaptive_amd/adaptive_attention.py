@@ -25,7 +25,6 @@ raises for B > 1) is not reproduced: the sampler uses the baseline's transpose s
 """
 from __future__ import annotations
 
-import collections
 import ctypes
 
 from typing import Dict, Optional, Tuple
@@ -162,39 +161,89 @@ class Decoder(nn.Module):
         return owner._decode_step(V, v_g, captions, states)
 
 
-class _Plan:
-    """An aa_decode_plan plus the buffers it was captured with (owned here, freed with it)."""
+class DecodePlan:
+    """A greedy decode of fixed (B, max_len) captured once into a hipGraph (C-ABI
+    ``aa_decode_plan_*``) over buffers the plan OWNS: its input ``images`` [B, C, 7, 7], its outputs
+    ``ids`` / ``alpha`` / ``beta`` and its workspace.  ``plan(x)`` copies ``x`` into the plan's own
+    input buffer (a device copy queued before the replay) and replays the graph; nothing of the
+    caller's is retained, so freshly allocated batches (the reference's eval loop,
+    code_src/tools/utils.py:167-171) never re-capture.  The outputs are the plan's buffers,
+    overwritten by the next replay (``clone()`` them to keep them).  Replays are bit-identical to
+    ``sampler``.  The plan binds the model's packed weights as they were when it was made; make a new
+    plan after the weights change (``plan.valid_for(model)``)."""
 
-    def __init__(self, lib, model, images, B, T, flags, n_lanes, cdims, dev):
-        self.lib = lib
-        self.images = images  # keep the captured input alive while the plan exists
-        self.ids = torch.empty(B, T, dtype=torch.int64, device=dev)
-        self.alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
-        self.beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
-        nbytes = lib.aa_decode_workspace_bytes(cdims, B, T)
-        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        h = ctypes.c_void_p()
-        with torch.cuda.device(dev):
-            torch.cuda.current_stream().synchronize()  # buffers allocated above are ready
-            _lib.check(lib.aa_decode_plan_create(model, images.data_ptr(), B, T, self.ids.data_ptr(),
+    def __init__(self, model: "Encoder2Decoder", B: int, max_len: int = 30, exact_vocab: bool = False,
+                 stream: Optional[torch.cuda.Stream] = None):
+        B, T = int(B), int(max_len)
+        if B <= 0 or T <= 0:
+            raise ValueError(f"DecodePlan needs B > 0 and max_len > 0, got B={B}, max_len={T}")
+        mstruct = model._model_struct()
+        lib = self.lib = _lib.load()
+        dev = self.device = model._packed.device
+        d = model.dims
+        self.B, self.T = B, T
+        self.flags = (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | model._decode_flags()
+        self._pack_ref = (model._packed.data_ptr(), model._pack_key)
+        self._packed = model._packed  # the graph reads the packed weights: keep them alive
+        self.stream = stream
+        with torch.cuda.device(dev), torch.cuda.stream(stream or torch.cuda.current_stream(dev)):
+            self.images = torch.empty(B, d.channels, 7, 7, dtype=torch.float32, device=dev)
+            self.ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+            self.alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+            self.beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+            nbytes = lib.aa_decode_workspace_bytes(model._c_dims(), B, T)
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            h = ctypes.c_void_p()
+            _lib.check(lib.aa_decode_plan_create(mstruct, self.images.data_ptr(), B, T, self.ids.data_ptr(),
                                                  self.alpha.data_ptr(), self.beta.data_ptr(), self.ws.data_ptr(),
-                                                 nbytes, flags, n_lanes, ctypes.byref(h)), "decode_plan_create")
+                                                 nbytes, self.flags, ctypes.byref(h)), "decode_plan_create")
         self.handle = h
+        self._done = None  # completion event of the last replay
+        Encoder2Decoder._captures += 1
 
-    def __del__(self):
+    def valid_for(self, model: "Encoder2Decoder") -> bool:
+        return model._packed is not None and (model._packed.data_ptr(), model._pack_key) == self._pack_ref
+
+    def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Replay the captured decode on ``stream`` (default: the plan's stream, else the current one)."""
+        s = stream or self.stream or torch.cuda.current_stream(self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.aa_decode_plan_launch(self.handle, s.cuda_stream), "decode_plan_launch")
+            ev = torch.cuda.Event()
+            ev.record(s)
+        self._done = ev
+
+    def __call__(self, images: Optional[torch.Tensor] = None):
+        s = self.stream or torch.cuda.current_stream(self.device)
+        if images is not None:
+            if tuple(images.shape) != tuple(self.images.shape) or images.dtype != torch.float32:
+                raise ValueError(f"DecodePlan: images must be {tuple(self.images.shape)} float32, got "
+                                 f"{tuple(images.shape)} {images.dtype}")
+            with torch.cuda.device(self.device), torch.cuda.stream(s):
+                self.images.copy_(images, non_blocking=True)
+        self.launch(s)
+        return self.ids, self.alpha, self.beta
+
+    def close(self) -> None:
+        """Destroy the graph once its last replay has completed (waits for that replay only)."""
         h = getattr(self, "handle", None)
         if h is not None and h.value:
-            try:
-                torch.cuda.synchronize()
-            except Exception:
-                pass
+            if self._done is not None:
+                self._done.synchronize()
             self.lib.aa_decode_plan_destroy(h)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Encoder2Decoder(nn.Module):
     """adaptive_attention.Encoder2Decoder on MI355X kernels."""
 
-    MAX_PLANS = 4
+    _captures = 0  # decode plans captured in this process (DecodePlan; sampler itself never captures)
 
     def __init__(self, cf, trunk: bool = False):
         """``trunk=True`` adds the ResNet-152 trunk (``encoder.resnet_conv``, keys as the
@@ -213,34 +262,20 @@ class Encoder2Decoder(nn.Module):
         self._pack_key = None
         self._packed = None
         self._model = None
-        self.decode_lanes = 1  # HIP streams the greedy step loop is split over (sampler(lanes=...))
         self.fp32_encoder = False  # True: V GEMM on fp32 MFMA instead of the fp32-accurate bf16x3 split
-        self.decode_graph = True  # replay repeated sampler calls from a captured hipGraph (aa_decode_plan)
-        # True: split each LSTM step into k_lstm_gemm (on a side stream, overlapping the previous
-        # step's attention / vocab stages) + k_lstm_cell -- same results, but measured slower than the
-        # one-launch k_lstm at B = 512 (cross-stream hand-offs cost more than the overlap gains;
-        # DESIGN.md §4), so off by default
-        self.split_lstm = False
-        # True: vocab screen on 64 x 64 tiles (k_vscreen) instead of 128 x 160 (k_vscreen2); same ids
-        self.screen64 = False
-        # True: the vocab screen appends per-row candidate lists against a running max lower bound
-        # (k_vscreen3) and k_vrescore3 rescores them, instead of granule summaries (k_vscreen2) +
-        # k_vrescore; same ids, measured slower at B = 512, so off by default
-        self.vocab_lists = False
-        # True: encoder V GEMM on k_enc_v3 (128 x 128 tiles) instead of k_enc_v4 (two images per
-        # workgroup, all columns: the feature map is read once); same accuracy class
-        self.enc_v3 = False
-        # True: beam-search vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256 (k_vbeam5);
-        # identical logits
-        self.beam_tile128 = False
         # True: teacher-forced training (forward()) with every GEMM on bf16 MFMA (bf16 operands, fp32
         # accumulation: BASELINE config 5); False: fp32 GEMMs
         self.train_bf16 = False
         # True: sampler() shards the batch over the ranks of the default torch.distributed group
         # (one process per GPU) and all-gathers the results (sharded_sampler); opt-in
         self.distributed_sampler = False
-        self._plans = collections.OrderedDict()  # key -> _Plan (LRU, MAX_PLANS)
-        self._plan_seen = set()
+        # sampler() over several GPUs of this process (the reference's sampler wraps the encoder in
+        # nn.DataParallel whenever torch.cuda.device_count() > 1, adaptive_attention.py:178-181):
+        # None = as the reference (every visible device when there is more than one, unless a
+        # multi-rank process group is initialised); False = this device only; True = every visible
+        # device; or a list of device indices (the first should be the images' device).
+        self.device_parallel = None
+        self._replicas = {}  # device index -> device_parallel._Replica
 
     # ---- weights -------------------------------------------------------------------------------
     def load_synthetic(self, seed: int = 123, bias_noise: float = 0.0) -> "Encoder2Decoder":
@@ -322,8 +357,6 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             _lib.check(lib.aa_pack_weights(model, w, _lib.stream_handle()), "pack_weights")
         self._packed, self._model, self._pack_key = packed, model, key
-        self._plans.clear()  # plans bind the packed buffer
-        self._plan_seen.clear()
         return model
 
     def _check_images(self, images: torch.Tensor) -> torch.Tensor:
@@ -339,78 +372,80 @@ class Encoder2Decoder(nn.Module):
     # ---- Encoder2Decoder.sampler (adaptive_attention.py:168-216) --------------------------------
     @torch.no_grad()
     def sampler(self, images: torch.Tensor, max_len: int = 30, trace: Optional[_lib.Trace] = None,
-                exact_vocab: bool = False, lanes: Optional[int] = None, graph: Optional[bool] = None):
+                exact_vocab: bool = False):
         """Greedy decode -> (ids [B,max_len] int64, alpha [B,max_len,49], beta [B,max_len,1]).
 
         ``exact_vocab=True`` computes every fp32 logit; the default screens with bf16 under a rigorous
-        error bound and rescores the candidates in exact fp32 — the ids are identical.
-        ``lanes`` (default ``self.decode_lanes``) splits the step loop over that many HIP streams by
-        row blocks so the lanes' kernels overlap; captions are independent, results are identical.
-        ``graph`` (default ``self.decode_graph``): repeated calls on the same input buffer replay a
-        captured hipGraph of the whole decode (C-ABI aa_decode_plan); results are identical.
+        error bound and rescores the candidates in exact fp32 -- the ids are identical.  Every call
+        launches the kernels directly on the current stream (about 4 max_len + 6 launches from one
+        C call); nothing is cached per input buffer and no caller tensor is retained after the call,
+        so a fresh batch per call (code_src/tools/utils.py:167-171) costs what a resident one does.
+        For repeated decodes of one shape, ``DecodePlan`` replays a captured hipGraph over its own
+        buffers.
+        Several GPUs in this process (``device_parallel``, default as the reference's
+        ``torch.cuda.device_count() > 1`` test, adaptive_attention.py:178-181): the rows are split
+        into contiguous blocks, one per device, decoded concurrently (device_parallel.py) and
+        gathered onto the images' device -- the same values as one decode of all rows.
         With ``self.distributed_sampler = True`` and an initialised multi-rank process group, every
-        rank passes the whole batch and the call runs ``sharded_sampler`` (the reference's sampler
-        distributes itself over the visible GPUs, adaptive_attention.py:178-181)."""
-        if self.distributed_sampler and trace is None:
+        rank passes the whole batch and the call runs ``sharded_sampler`` (one process per GPU)."""
+        if trace is None:
             import torch.distributed as dist
-            if dist.is_initialized() and dist.get_world_size() > 1:
-                return self.sharded_sampler(images, max_len, exact_vocab=exact_vocab, lanes=lanes, graph=graph)
-        return self._sampler_local(images, max_len, trace, exact_vocab, lanes, graph)
+            multi_rank = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            if self.distributed_sampler and multi_rank:
+                return self.sharded_sampler(images, max_len, exact_vocab=exact_vocab)
+            devices = self._parallel_devices(images, multi_rank)
+            if devices is not None:
+                from .device_parallel import parallel_sampler
+                return parallel_sampler(self, images, int(max_len), devices, exact_vocab=exact_vocab)
+        return self._sampler_local(images, max_len, trace, exact_vocab)
+
+    def _parallel_devices(self, images: torch.Tensor, multi_rank: bool):
+        """Device indices for a single-process multi-device decode, or None (this device only)."""
+        mode = self.device_parallel
+        if mode is False or not images.is_cuda:
+            return None
+        if mode is None:  # as the reference: every visible device when there are several
+            if multi_rank or torch.cuda.device_count() < 2:
+                return None
+            mode = True
+        home = images.device.index if images.device.index is not None else torch.cuda.current_device()
+        if mode is True:
+            devs = [home] + [d for d in range(torch.cuda.device_count()) if d != home]
+        else:
+            devs = [int(d) for d in mode]
+        return devs if len(devs) > 1 else None
 
     @torch.no_grad()
-    def _sampler_local(self, images, max_len, trace=None, exact_vocab=False, lanes=None, graph=None):
+    def _sampler_local(self, images, max_len, trace=None, exact_vocab=False):
         images = self._check_images(self.features(images))
-        model = self._model_struct()
-        lib = _lib.load()
         B, T, dev = images.size(0), int(max_len), images.device
-        n = int(self.decode_lanes if lanes is None else lanes)
-        if not 1 <= n <= _lib.MAX_LANES:
-            raise ValueError(f"lanes must be in [1, {_lib.MAX_LANES}], got {n}")
-        flags = ((_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
-                 | self._lstm_flags())
-        use_graph = self.decode_graph if graph is None else bool(graph)
-        if use_graph and trace is None and B > 0 and T > 0:
-            # A plan binds the images pointer; it is captured the second time a key is seen, so
-            # one-off calls never pay for a capture.
-            key = (dev.index, images.data_ptr(), B, T, flags, n, self._packed.data_ptr())
-            plan = self._plans.get(key)
-            if plan is None and key in self._plan_seen:
-                plan = self._plans[key] = _Plan(lib, model, images, B, T, flags, n, self._c_dims(), dev)
-                while len(self._plans) > self.MAX_PLANS:
-                    self._plans.popitem(last=False)
-            if plan is not None:
-                self._plans.move_to_end(key)
-                with torch.cuda.device(dev):
-                    _lib.check(lib.aa_decode_plan_launch(plan.handle, _lib.stream_handle()), "decode_plan_launch")
-                return plan.ids.clone(), plan.alpha.clone(), plan.beta.clone()
-            if len(self._plan_seen) > 64:
-                self._plan_seen.clear()
-            self._plan_seen.add(key)
         ids = torch.empty(B, T, dtype=torch.int64, device=dev)
         alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
         beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+        self._decode_into(images, T, ids, alpha, beta, trace=trace, exact_vocab=exact_vocab)
+        return ids, alpha, beta
+
+    def _decode_into(self, images, T, ids, alpha, beta, trace=None, exact_vocab=False, stream=None):
+        """aa_greedy_decode_aux of ``images`` [B,C,7,7] (checked, on the model's device) into the
+        given contiguous outputs, on ``stream`` (default: the current stream)."""
+        model = self._model_struct()
+        lib = _lib.load()
+        B, dev = images.size(0), images.device
+        flags = (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | self._decode_flags()
         ws = self._workspace(lib.aa_decode_workspace_bytes(self._c_dims(), B, T), dev)
         with torch.cuda.device(dev):
-            if n == 1:
-                # second stream: the encoder's a_g branch and the next step's h W_hh^T run beside the chain
-                aux = self._aux_stream(dev)
-                aux.wait_stream(torch.cuda.current_stream())  # (the library forks/joins through events too)
-                rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                              beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                              trace, flags, _lib.stream_handle(),
-                                              aux.cuda_stream)
-            else:
-                handles = (ctypes.c_void_p * n)(*[st.cuda_stream for st in self._lanes(n, dev)])
-                rc = lib.aa_greedy_decode_lanes(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                                beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                                trace, flags, _lib.stream_handle(), handles, n)
+            s = stream or torch.cuda.current_stream(dev)
+            # second stream: the encoder's a_g branch (heads, x_g) runs beside the VWv GEMM
+            aux = self._aux_stream(dev)
+            aux.wait_stream(s)  # (the library forks/joins through events too)
+            rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                          beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                                          trace, flags, s.cuda_stream, aux.cuda_stream)
         _lib.check(rc, "greedy_decode")
-        return ids, alpha, beta
 
     @torch.no_grad()
     def sharded_sampler(self, images: torch.Tensor, max_len: int = 30, total: Optional[int] = None, group=None,
-                        gather_attention: bool = True, exact_vocab: bool = False, lanes: Optional[int] = None,
-                        graph: Optional[bool] = None):
+                        gather_attention: bool = True, exact_vocab: bool = False):
         """Multi-rank ``sampler``: the one-process-per-GPU counterpart of the reference's
         self-distributing sampler (``nn.DataParallel`` over every visible GPU,
         adaptive_attention.py:178-181).  Every rank of ``group`` (``torch.distributed``; ``nccl`` =
@@ -419,8 +454,7 @@ class Encoder2Decoder(nn.Module):
         returns the whole batch's results on every rank -- the same values as one ``sampler`` call
         over all rows (rows never interact, and no kernel's per-row arithmetic depends on the batch
         size).  ``images``: the full batch on every rank (``total=None``), or this rank's block of a
-        ``total``-row batch.  ``exact_vocab``, ``lanes`` and ``graph`` apply to each rank's local
-        decode as in ``sampler``."""
+        ``total``-row batch.  ``exact_vocab`` applies to each rank's local decode as in ``sampler``."""
         import torch.distributed as dist
         from . import distributed as D
         if not dist.is_initialized():
@@ -429,7 +463,7 @@ class Encoder2Decoder(nn.Module):
             total = images.size(0)
             images = D.local_rows(images, group)
         def local(x, t):
-            return self._sampler_local(x, t, exact_vocab=exact_vocab, lanes=lanes, graph=graph)
+            return self._sampler_local(x, t, exact_vocab=exact_vocab)
 
         ids, alpha, beta = D.sharded_sampler(local, images, int(total), int(max_len),
                                              group=group, gather_attention=gather_attention)
@@ -475,43 +509,25 @@ class Encoder2Decoder(nn.Module):
             rc = lib.aa_beam_decode(model, images.data_ptr(), B, T, K, int(end_id), ids.data_ptr(), seqs.data_ptr(),
                                     scores.data_ptr(), alpha.data_ptr(), beta.data_ptr(), _lib.ptr(ws),
                                     ws.numel() if ws is not None else 0,
-                                    (_lib.BEAM_FAST if fast else 0) | (_lib.DECODE_EXACT_VOCAB if check else 0)
-                                    | (_lib.BEAM_TILE128 if self.beam_tile128 else 0), _lib.stream_handle(),
+                                    (_lib.BEAM_FAST if fast else 0) | (_lib.DECODE_EXACT_VOCAB if check else 0),
+                                    _lib.stream_handle(),
                                     vocab_events)
         _lib.check(rc, "beam_decode")
         return ids, alpha, beta, seqs, scores
 
     def _aux_stream(self, dev) -> torch.cuda.Stream:
-        """The side stream of ``aa_greedy_decode_aux`` on ``dev`` (created once, reused): a fresh HIP
-        stream (hip_events.new_raw_stream), so it takes its own hardware queue in HIP's round-robin
-        instead of a torch pool stream whose queue may be the caller's."""
-        cache = self.__dict__.setdefault("_aux_streams", {})
-        key = dev.index if dev.index is not None else torch.cuda.current_device()
-        if key not in cache:
-            from .hip_events import new_raw_stream
-            cache[key] = new_raw_stream(dev)
-        return cache[key]
+        """The side stream of ``aa_greedy_decode_aux`` on ``dev``: the process's "decode-aux" role
+        stream (hip_events.role_stream: a fresh HIP stream on its own hardware queue, shared by every
+        model, so building models in a loop creates no further streams)."""
+        from .hip_events import role_stream
+        return role_stream(dev, "decode-aux")
 
     def _train_flags(self) -> int:
         return _lib.TRAIN_BF16 if getattr(self, "train_bf16", False) else 0
 
     def _decode_flags(self) -> int:
         """Flags of a default greedy decode (what sampler passes without exact_vocab)."""
-        return (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0) | self._lstm_flags()
-
-    def _lstm_flags(self) -> int:
-        return ((0 if self.split_lstm else _lib.DECODE_FUSED_LSTM) | (_lib.DECODE_SCREEN64 if self.screen64 else 0)
-                | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0) | (_lib.DECODE_LISTS if self.vocab_lists else 0))
-
-    def _lanes(self, n: int, dev) -> list:
-        """n side streams on ``dev`` (created once, reused; fresh HIP streams, as ``_aux_stream``)."""
-        from .hip_events import new_raw_stream
-        cache = self.__dict__.setdefault("_lane_streams", {})
-        key = (dev.index if dev.index is not None else torch.cuda.current_device())
-        have = cache.setdefault(key, [])
-        while len(have) < n:
-            have.append(new_raw_stream(dev))
-        return have[:n]
+        return _lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0
 
     def _workspace(self, nbytes: int, dev) -> Optional[torch.Tensor]:
         if nbytes == 0:
@@ -538,8 +554,7 @@ class Encoder2Decoder(nn.Module):
         with torch.cuda.device(dev):
             rc = lib.aa_encoder_tail(model, images.data_ptr(), B, a_g.data_ptr(), V.data_ptr(), v_g.data_ptr(),
                                      h0.data_ptr(), c0.data_ptr(), VWv.data_ptr(),
-                                     (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0)
-                                     | (_lib.DECODE_ENC_V3 if self.enc_v3 else 0), _lib.stream_handle())
+                                     _lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0, _lib.stream_handle())
         _lib.check(rc, "encoder_tail")
         return V, v_g, (h0, c0), a_g, VWv
 

@@ -687,7 +687,7 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
     hipLaunchKernelGGL(k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, L.Vp, w.u3, \
                        p.mlp_w3, p.mlp_b, w.logits, w.gsum)
       // 256 x 256 tiles when the padded vocabulary is whole 256-column tiles (V = 10,123: 40 of them)
-      const bool wide = L.Vp % 256 == 0 && !(flags & AA_BEAM_TILE128);
+      const bool wide = L.Vp % 256 == 0;  // else 128 x 128 tiles (k_vbeam4)
       switch (H) {
         case 256: AA_VB3(256); break;
         case 512: AA_VB3(512); break;

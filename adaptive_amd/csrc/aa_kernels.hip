@@ -50,9 +50,6 @@ constexpr float CEPS = 0.0085f;
 constexpr float EPS_ABS = 1e-5f;
 constexpr int VS_TILE = 32;     // screen summary granule: one (lbmax, top-2 ub) per row per 32 columns
 constexpr int RS_CAP = 2048;    // candidate list capacity per row in k_vrescore (else full row)
-constexpr int LCAP = 64;        // k_vscreen3 -> k_vrescore3 list entries per row and step (else full row)
-constexpr int MK_LD = 1;        // row pitch of k_vscreen3's running lower bounds (uint32)
-constexpr int LCNT_LD = 1;      // row pitch of its list counts (uint32)
 // Exact fp32 logits (k_vocab and the rescoring) are NP_VOCAB independent fma chains over contiguous
 // K ranges (in the MFMA k order), combined as ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)), then + bias.
 constexpr int NP_VOCAB = 8;
@@ -915,160 +912,6 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
   }
 }
 
-// GEMM main loop shared by k_lstm and k_lstm_gemm: wave w accumulates the 64x64 tile (2 x 2 blocks
-// of 32x32) over its K chunks [w KC/8, (w+1) KC/8) from fragments af0/af1 (the tile's two 32-row
-// blocks of split h) and wf0/wf1 (its two 32-column blocks of split W_hh), two chunks in flight;
-// then the eight partial tiles are summed in LDS: waves 4..7 store, waves 0..3 add theirs and store
-// q_w = p_w + p_(w+4) into slot w (tiles stored transposed, [column][row] with pitch LS_CP: a lane's
-// 4 consecutive accumulator rows are one 16-B access).  The caller finishes the fixed tree
-// ((q0 + q1) + (q2 + q3)) after a barrier.  `between` runs after the first loads are issued
-// (token-dependent gathers of k_lstm).
-template <int H, class F>
-__device__ __forceinline__ void lstm_gemm_partials(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
-                                                   const bf16x8* wf1, float* Pt, F&& between) {
-  constexpr int KC = H / 16, CP = LS_CP, TS = 64 * LS_CP;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  constexpr int per = KC / 8;  // even for H in {256, 512, 768, 1024}
-  const int kc0 = wave * per;
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-  bf16x8 fa[2][2][3], fw[2][2][3];  // [slot][block][plane]
-  auto load = [&](int slot, int kc) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const size_t o = ((size_t)kc * 3 + q) * 64;
-      fa[slot][0][q] = af0[o];
-      fa[slot][1][q] = af1[o];
-      fw[slot][0][q] = wf0[o];
-      fw[slot][1][q] = wf1[o];
-    }
-  };
-  const int last = kc0 + per - 1;
-  asm volatile("" ::: "memory");
-  load(0, kc0);
-  load(1, kc0 + 1 < last ? kc0 + 1 : last);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  between();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < per; i += 2) {
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) x3_step(acc[a][c], fa[d][a], fw[d][c]);
-      const int nk = kc0 + i + d + 2;
-      load(d, nk < last ? nk : last);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  float* dst = Pt + (wave & 3) * TS;
-  const int li = lane & 31, lh = lane >> 5;
-  if (wave >= 4) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          *reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh) =
-              make_float4(acc[a][c][4 * r4], acc[a][c][4 * r4 + 1], acc[a][c][4 * r4 + 2], acc[a][c][4 * r4 + 3]);
-  }
-  __syncthreads();
-  if (wave < 4) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          float4* e = reinterpret_cast<float4*>(dst + (c * 32 + li) * CP + a * 32 + 8 * r4 + 4 * lh);
-          const float4 v = *e;
-          *e = make_float4(acc[a][c][4 * r4] + v.x, acc[a][c][4 * r4 + 1] + v.y, acc[a][c][4 * r4 + 2] + v.z,
-                           acc[a][c][4 * r4 + 3] + v.w);
-        }
-  }
-}
-
-// Lean variant of lstm_gemm_partials (k_lstm<.., LEAN = true>): wave w owns ONE 32x32 block
-// (a = (w >> 1) & 1, c = w & 1) over one K half (w >> 2), a 2-chunk fragment ring, so the
-// workgroup needs ~half the VGPRs and one LDS tile instead of four: two workgroups fit on a CU
-// (one from each batch in flight) where the 8-partial version claims the whole CU.  Each fragment
-// is loaded by the two waves that share it (twice the L2 reads).  The K halves are summed as
-// (lower + upper) into the single tile Pt [column][row]; the caller reads it after a barrier.
-#ifndef AA_LSTM_NR
-#define AA_LSTM_NR 2
-#endif
-#ifndef AA_LSTM_OCC
-#define AA_LSTM_OCC 4
-#endif
-template <int H, class F>
-__device__ __forceinline__ void lstm_gemm_lean(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
-                                               const bf16x8* wf1, float* Pt, F&& between) {
-  constexpr int KC = H / 16, CP = LS_CP, per = KC / 2, NR = AA_LSTM_NR;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
-  const bf16x8* af = a ? af1 : af0;
-  const bf16x8* wf = c ? wf1 : wf0;
-  const int kc0 = kh * per;
-  floatx16 acc, acc2;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
-  bf16x8 fa[NR][3], fw[NR][3];
-  auto load = [&](int slot, int kc) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const size_t o = ((size_t)kc * 3 + q) * 64;
-      fa[slot][q] = af[o];
-      fw[slot][q] = wf[o];
-    }
-  };
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < NR; ++i) load(i, kc0 + i);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  between();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < per; ++i) {
-#ifdef AA_EXP_NOMFMA  // tools/ktrace experiment: loads only (wrong results)
-    acc[0] += (float)fa[i % NR][0][0] + (float)fw[i % NR][0][0];
-#else
-    x3_step2(acc2, acc, fa[i % NR], fw[i % NR]);
-#endif
-#ifndef AA_EXP_NOLOAD  // tools/ktrace experiment: MFMAs on the first NR chunks only (wrong results)
-    if (i + NR < per) load(i % NR, kc0 + i + NR);
-#endif
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] += acc2[r];  // large-product chain + small-product chain
-  const int li = lane & 31, lh = lane >> 5;
-  float* dst = Pt + (c * 32 + li) * CP + a * 32 + 4 * lh;
-  if (kh) {
-#pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4)
-      *reinterpret_cast<float4*>(dst + 8 * r4) = make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
-  }
-  __syncthreads();
-  if (!kh) {
-#pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-      float4* e = reinterpret_cast<float4*>(dst + 8 * r4);
-      const float4 v = *e;
-      *e = make_float4(acc[4 * r4] + v.x, acc[4 * r4 + 1] + v.y, acc[4 * r4 + 2] + v.z, acc[4 * r4 + 3] + v.w);
-    }
-  }
-}
-
 // LDS-staged variant of the lean GEMM (the default): the same waves, blocks, K halves, chunk order
 // and MFMA sequence (bit-identical accumulators), but every fragment reaches LDS ONCE per workgroup by
 // LDS-DMA (global_load_lds, 1 KB per wave instruction) and the two waves that share it read it
@@ -1155,16 +998,10 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
       vm_wait(3 * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0));
       // every wave's stage-it reads retired (lgkmcnt) before any wave refills that buffer
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#ifndef AA_EXP_NOLOAD
       if (it + NB < N) issue(it + NB);
-#endif
       lread(it + 1, set ^ 1);
     }
-#ifdef AA_EXP_NOMFMA
-    acc[0] += (float)fa[set][0][0] + (float)fw[set][0][0];
-#else
     x3_step2(acc2, acc, fa[set], fw[set]);
-#endif
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
@@ -1191,8 +1028,11 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
 // G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
 // fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
 // gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
-template <int H, bool G = false, bool LEAN = true>
-__global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
+#ifndef AA_LSTM_OCC
+#define AA_LSTM_OCC 4
+#endif
+template <int H, bool G = false>
+__global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
                                               const float* __restrict__ c_in, const int* __restrict__ par,
@@ -1202,10 +1042,10 @@ __global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int
                                               float* __restrict__ s_out, float* __restrict__ part) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
   AA_TS(0, 0);
-  // LEAN: the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
+  // the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
   constexpr int RING_FLOATS = (LS_NB < H / 32 ? LS_NB : H / 32) * LS_STAGE * 4;
-  constexpr int LDS_FLOATS = LEAN ? RING_FLOATS + 64 : 4 * TS + LS_TAIL_FLOATS;  // + the tile's 64 tokens
-  static_assert(!LEAN || TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
+  constexpr int LDS_FLOATS = RING_FLOATS + 64;  // + the tile's 64 tokens
+  static_assert(TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
@@ -1221,17 +1061,13 @@ __global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int
   //  then waits for the token alone; the asm barriers keep the compiler from reordering the loads)
   int64_t tk = 0;
   int* tok_lds = reinterpret_cast<int*>(lds + RING_FLOATS);
-  if constexpr (LEAN) {
-    // the tile's 64 tokens by ONE LDS-DMA of wave 0 (the low dword of each int64 token), so that no
-    // ordinary load is outstanding beside the ring's DMAs: hipcc drains every DMA (vmcnt(0)) before
-    // the first use of an ordinary load's result while a DMA is in flight
-    if (t < 64) {
-      const int r = m0 + t < B ? m0 + t : B - 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tok + (int64_t)r * tok_ld),
-                                       (__attribute__((address_space(3))) void*)tok_lds, 4, 0, 0);
-    }
-  } else {
-    tk = tok[(int64_t)mc * tok_ld];
+  // the tile's 64 tokens by ONE LDS-DMA of wave 0 (the low dword of each int64 token), so that no
+  // ordinary load is outstanding beside the ring's DMAs: hipcc drains every DMA (vmcnt(0)) before
+  // the first use of an ordinary load's result while a DMA is in flight
+  if (t < 64) {
+    const int r = m0 + t < B ? m0 + t : B - 1;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tok + (int64_t)r * tok_ld),
+                                     (__attribute__((address_space(3))) void*)tok_lds, 4, 0, 0);
   }
   const bf16x8* af0;
   const bf16x8* af1;
@@ -1269,36 +1105,19 @@ __global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int
     const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
     wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
   };
-  if constexpr (LEAN) {
-    // token first (oldest), then the ring's first three stages, then -- once the token is in --
-    // the token-dependent gathers (exactly LS_GATHERS loads, counted by the ring's waits)
+  // token first (oldest), then the ring's first three stages, then -- once the token is in --
+  // the token-dependent gathers (exactly LS_GATHERS loads, counted by the ring's waits)
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
+    // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
+    if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    tk = tok_lds[rr];
+    gathers();
     asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
-      // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
-      if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      tk = tok_lds[rr];
-      gathers();
-      asm volatile("" ::: "memory");
-    });
-    AA_TS(0, 1);
-  } else {
-    lstm_gemm_partials<H>(af0, af1, wf0, wf1, Pt, gathers);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {  // 512 threads x 2 float4 = the 64 x 64 tile
-      const int q = t + 512 * i, cq = q >> 4, r4 = (q & 15) * 4;
-      const float* sp = Pt + cq * CP + r4;
-      float4 v[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) v[w] = *reinterpret_cast<const float4*>(sp + w * TS);
-      float4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) (&o.x)[e] = (f4c(v[0], e) + f4c(v[1], e)) + (f4c(v[2], e) + f4c(v[3], e));
-      *reinterpret_cast<float4*>(Pt + cq * CP + r4) = o;
-    }
-  }
+  });
+  AA_TS(0, 1);
   __syncthreads();
   float gate[4][2];
   {
@@ -1309,111 +1128,22 @@ __global__ __launch_bounds__(512, LEAN ? AA_LSTM_OCC : 1) void k_lstm(int B, int
       for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
   }
   AA_TS(0, 2);
-  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + (LEAN ? 1 : 4) * TS, h_out, hsp_out, c_out, s_out, part);
+  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + TS, h_out, hsp_out, c_out, s_out, part);
   AA_TS(0, 4);
-}
-
-// Split LSTM step, part 1: G = h_{t-1} W_hh^T (the tile of k_lstm, same lean partials and order) written
-// to gates [B][H/16 tiles][8 unit pairs][4 gates][2 units] -- the order k_lstm_cell's threads read
-// (two float4 each).  Depends only on h_{t-1}, so the decode loop runs it on a second stream beside
-// the previous step's attention, vocab screen and rescoring (the token is not needed here).
-template <int H>
-__global__ __launch_bounds__(512, 4) void k_lstm_gemm(int B, const bf16x8* __restrict__ hsp_in,
-                                                   const bf16x8* __restrict__ whh3, float* __restrict__ gates) {
-  constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP, NTn = H / 16, KC = H / 16;
-  __shared__ __attribute__((aligned(16))) float Pt[TS];
-  const int MT = (B + BM - 1) / BM;
-  const int L = xcd_remap(blockIdx.x, MT * NTn);
-  const int nt = L / MT, mt = L % MT;
-  const int t = threadIdx.x, lane = t & 63;
-  const int m0 = mt * BM;
-  const bf16x8* af0 = hsp_in + (size_t)(m0 / 32) * KC * 3 * 64 + lane;
-  const bf16x8* af1 = af0 + (size_t)KC * 3 * 64;
-  const bf16x8* wf0 = whh3 + (size_t)(nt * 2) * KC * 3 * 64 + lane;
-  const bf16x8* wf1 = wf0 + (size_t)KC * 3 * 64;
-  lstm_gemm_lean<H>(af0, af1, wf0, wf1, Pt, [] {});
-  __syncthreads();
-  const int rr = t >> 3, pp = t & 7, m = m0 + rr;
-  float o[8];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const float* sp = Pt + (16 * g + 2 * pp + q) * CP + rr;
-      o[2 * g + q] = sp[0];
-    }
-  if (m < B) {
-    float4* dst = reinterpret_cast<float4*>(gates + (((int64_t)m * NTn + nt) * 8 + pp) * 8);
-    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
-  }
-}
-
-// Split LSTM step, part 2: the cell of k_lstm on G from k_lstm_gemm (bit-identical to k_lstm).
-// G (beam search): row m continues row par[m]: its GEMM row and c come from that row.
-template <int H, bool G = false>
-__global__ __launch_bounds__(512) void k_lstm_cell(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
-                                                   const float* __restrict__ table, const float* __restrict__ xg,
-                                                   const float* __restrict__ gates, const float* __restrict__ c_in,
-                                                   const int* __restrict__ par, const float* __restrict__ wgs,
-                                                   float* __restrict__ h_out, bf16x8* __restrict__ hsp_out,
-                                                   float* __restrict__ c_out, float* __restrict__ s_out,
-                                                   float* __restrict__ part) {
-  constexpr int BM = 64, NTn = H / 16;
-  __shared__ __attribute__((aligned(16))) float lds[LS_TAIL_FLOATS];
-  const int MT = (B + BM - 1) / BM;
-  const int L = xcd_remap(blockIdx.x, MT * NTn);
-  const int nt = L / MT, mt = L % MT;
-  const int t = threadIdx.x, m0 = mt * BM;
-  const int rr = t >> 3, pp = t & 7, u0 = 2 * pp, m = m0 + rr;
-  const int mc = m < B ? m : B - 1;
-  const int j = nt * 16 + u0;
-  int64_t tk = tok[(int64_t)mc * tok_ld];
-  const int pc = G ? par[mc] : mc;
-  const float4* gsrc = reinterpret_cast<const float4*>(gates + (((int64_t)pc * NTn + nt) * 8 + pp) * 8);
-  const float4 g0 = gsrc[0], g1 = gsrc[1];
-  const float2 cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
-  const float4* wsrc = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
-  const float4 wsv = wsrc[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
-  const int N5 = 5 * H;
-  const float* xrow = xg + (int64_t)mc * N5;
-  float2 xa[4], ta[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
-  const float2 sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
-  tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
-  const float* trow = table + tk * N5;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
-  const float2 sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
-  const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-  float gate[4][2];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) gate[g][q] = gv[2 * g + q] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
-  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds, h_out, hsp_out, c_out, s_out, part);
 }
 
 __global__ void k_fill_tok(int64_t* __restrict__ tok, int B, int64_t v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B) tok[i] = v;
 }
-// Start of a greedy decode: <start> tokens, and the [T][B] argmax keys and running lower bounds
-// that k_vscreen3 accumulates by atomicMax cleared.
-// Start of a greedy decode: <start> tokens, and the [T][B] arrays that the vocab stage accumulates
-// into by atomics cleared -- argmax keys (k_vocab), running lower bounds and list counts
-// (k_vscreen3) -- by memory-side stores, like the atomics that follow (a plain store's line would
-// stay in this XCD's L2)
-__global__ void k_decode_init(int64_t* __restrict__ tok, int B, int64_t v, uint64_t* __restrict__ keys,
-                              uint32_t* __restrict__ mk, uint32_t* __restrict__ lcnt, int n) {
+// Start of a greedy decode: <start> tokens, and (exact vocab stage) the [T][B] argmax keys that
+// k_vocab accumulates by atomicMax cleared -- by memory-side stores, like the atomics that follow (a
+// plain store's line would stay in this XCD's L2)
+__global__ void k_decode_init(int64_t* __restrict__ tok, int B, int64_t v, uint64_t* __restrict__ keys, int n) {
   const int i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   for (int i = i0; i < B; i += stride) tok[i] = v;
-  for (int i = i0; i < n; i += stride) {  // (each array only when the decode's vocab stage uses it)
-    if (keys) __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (mk) __hip_atomic_store(mk + (int64_t)i * MK_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lcnt) __hip_atomic_store(lcnt + (int64_t)i * LCNT_LD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (keys)
+    for (int i = i0; i < n; i += stride) __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void k_key_ids(const uint64_t* __restrict__ keys, int B, int64_t* __restrict__ ids, int ld) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2194,7 +1924,7 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
   }
 }
 
-// Main loop of the wide screen (k_vscreen2 / k_vscreen3): the tile's screened products
+// Main loop of the wide screen (k_vscreen2): the tile's screened products
 // acc[b] = bf16(u) . bf16(w) of wave w's 32 rows x column block b (no bias), and un_s = ||u|| of the
 // tile's 128 rows.
 template <int H>
@@ -2309,127 +2039,6 @@ __global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const
     screen_block_summ(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
   }
 #endif
-  AA_TS(2, 2);
-}
-
-// Screen, LDS-DMA form (k_vscreen4, AA_SCREEN_DMA=1 builds; measured slower, so not the default):
-// k_vscreen2's tile, waves, MFMA order and
-// epilogue (bit-identical summaries), but every operand reaches LDS by LDS-DMA (global_load_lds, 1 KB
-// per wave instruction) into an SC4_NB-slot ring, with no register staging, no ds_write and no
-// ordinary global load in flight beside the DMAs (hipcc would drain the DMAs before the first use of
-// one).  A stage = SC2_KS k16 chunks of the tile's 4 u row blocks and 5 W column blocks = 36 fragments
-// (36 KB), 9 issued by each wave; SC4_NB - 1 stages stay in flight while one is multiplied.  The
-// epilogue's operands (||u|| of the 128 rows, the 160 biases, the 5 granule bound factors) arrive by
-// one more DMA per wave before the ring, so the whole kernel has no exposed round trip but the ring's.
-// Measured (round 3, A/B of two builds on one box, two rounds, HIP events): k_vscreen2 14.4 / 14.2 us,
-// k_vscreen4 15.5 / 16.0 us (3-slot ring 15.9 / 15.8); parity green (bit-identical summaries).  The
-// 36 LDS-DMA wave instructions per stage cost more issue time than the register staging they replace:
-// the screen's main loop is not bound by its bytes in flight.
-#ifndef AA_SCREEN_DMA
-#define AA_SCREEN_DMA 0
-#endif
-#ifndef AA_SC4_NB
-#define AA_SC4_NB 4
-#endif
-constexpr int SC4_NB = AA_SC4_NB, SC4_FPW = (4 + SC2_NB) * SC2_KS / 4;  // ring slots; fragments per wave per stage
-constexpr int SC4_STAGE = 4 * SC4_FPW * 64;                             // bf16x8 per stage
-static_assert(SC4_FPW * 4 == (4 + SC2_NB) * SC2_KS, "a stage's fragments split evenly over the 4 waves");
-
-template <int H>
-__global__ __launch_bounds__(256, 1) void k_vscreen4(int B, int V, int Vp, const bf16x8* __restrict__ ua,
-                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
-                                                  float4* __restrict__ summ) {
-  constexpr int KC = H / 16, NS = KC / SC2_KS, NB = SC4_NB < NS ? SC4_NB : NS;
-  static_assert(NB >= 2, "the ring needs two slots");
-  __shared__ __attribute__((aligned(16))) bf16x8 ring[NB * SC4_STAGE];
-  __shared__ __attribute__((aligned(16))) float ep[SC2_BM + 4 * 64 + 64];  // ||u|| [128], bias [256], gs [64]
-  AA_TS(2, 0);
-  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
-  const int L = xcd_remap(blockIdx.x, MT * NT);
-  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
-  // epilogue operands, one DMA per wave (lanes past the end re-read the last valid element)
-  typedef __attribute__((address_space(3))) void lds_t;
-  if (wave < 2) {  // ||u|| of rows m0 + 64 wave + lane
-    const int r = m0 + 64 * wave + lane;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(unorm + (r < B ? r : B - 1)),
-                                     (lds_t*)(ep + 64 * wave), 4, 0, 0);
-  } else if (wave == 2) {  // the 160 biases as 40 float4
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(bias + n0 + 4 * (lane < 40 ? lane : 39)),
-                                     (lds_t*)(ep + SC2_BM), 16, 0, 0);
-  } else {  // the 5 granules' (max ||w||, max |b|) as 10 floats
-    const float* g = reinterpret_cast<const float*>(gs + n0 / VS_TILE);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + (lane < 2 * SC2_NB ? lane : 2 * SC2_NB - 1)),
-                                     (lds_t*)(ep + SC2_BM + 256), 4, 0, 0);
-  }
-  // fragment f of a stage: f < 16 -> u row block f / 4, chunk f % 4; else W column block (f - 16) / 4,
-  // chunk (f - 16) % 4; wave w issues f = 9 w .. 9 w + 8; stage s adds 4 s chunks
-  const bf16x8* src[SC4_FPW];
-#pragma unroll
-  for (int i = 0; i < SC4_FPW; ++i) {
-    const int f = SC4_FPW * wave + i;
-    src[i] = f < 16 ? ua + ((size_t)((m0 >> 5) + f / 4) * KC + f % 4) * 64 + lane
-                    : wf + ((size_t)((n0 >> 5) + (f - 16) / 4) * KC + (f - 16) % 4) * 64 + lane;
-  }
-  auto issue = [&](int s) {
-    bf16x8* dst = ring + (s % NB) * SC4_STAGE + SC4_FPW * wave * 64;
-#pragma unroll
-    for (int i = 0; i < SC4_FPW; ++i)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)s * SC2_KS * 64),
-                                       (lds_t*)(dst + i * 64), 16, 0, 0);
-  };
-  // chunk c of stage s into register set: this wave's u fragment and the 5 W fragments
-  bf16x8 fa[2], fw[2][SC2_NB];
-  auto lread = [&](int s, int c, int set) {
-    const bf16x8* sb = ring + (s % NB) * SC4_STAGE + lane;
-    fa[set] = sb[(4 * wave + c) * 64];
-#pragma unroll
-    for (int b = 0; b < SC2_NB; ++b) fw[set][b] = sb[(16 + 4 * b + c) * 64];
-  };
-  floatx16 acc[SC2_NB];
-#pragma unroll
-  for (int b = 0; b < SC2_NB; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int s = 0; s < NB; ++s) issue(s);
-  __builtin_amdgcn_sched_barrier(0);
-  // stage 0 landed (younger: stages 1 .. NB-1); the epilogue DMA is older
-  vm_wait(SC4_FPW * (NB - 1));
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  lread(0, 0, 0);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-#pragma unroll
-    for (int c = 0; c < SC2_KS; ++c) {
-      const int set = c & 1;
-      if (c + 1 < SC2_KS) {
-        lread(s, c + 1, set ^ 1);
-      } else if (s + 1 < NS) {
-        // stage s + 1 landed: younger are the stages issued after it (up to s + NB - 1)
-        const int last = s + NB - 1 < NS - 1 ? s + NB - 1 : NS - 1;
-        vm_wait(SC4_FPW * (last - (s + 1)));
-        // every wave's reads of stage s retired before its slot is refilled
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (s + NB < NS) issue(s + NB);
-        lread(s + 1, 0, set ^ 1);
-      }
-#pragma unroll
-      for (int b = 0; b < SC2_NB; ++b)
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set], fw[set][b], acc[b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  AA_TS(2, 1);
-  float bvs[SC2_NB];
-#pragma unroll
-  for (int b = 0; b < SC2_NB; ++b) bvs[b] = ep[SC2_BM + 32 * b + (lane & 31)];
-  screen_blocks_summ<SC2_NB>(acc, m0 + 32 * wave, n0 / VS_TILE, bvs,
-                             reinterpret_cast<const float2*>(ep + SC2_BM + 256), ep + 32 * wave, n0, V, B, NTn, summ);
   AA_TS(2, 2);
 }
 
@@ -2552,220 +2161,6 @@ __global__ __launch_bounds__(RS_NT) void k_vrescore(int B, int V, int Vp, const 
 }
 
 // ---------------------------------------------------------------------------------------------
-// D3 (greedy path, AA_DECODE_LISTS): the wide screen writes per-row candidate LISTS instead of
-// per-granule summaries, and k_vrescore3 rescores each row's short list.  The summaries' path
-// (k_vscreen2 + k_vrescore, the default) reads 320 summaries per row to find M and then expands a
-// granule whose second-best bound reaches M to all 32 of its columns; here the screen decides per
-// column, against a running M (measured: the epilogue's atomic round trips -- publish/read M, claim
-// list slots -- cost more than the summaries' scan and expansion save):
-//   1. per row of the tile: lb = max over the tile's columns of A_n - E (the screen's bound, CEPS),
-//      published by an atomicMax into mk[row] (order-preserving u32 keys); the returned value gives
-//      M_cur = max of every lb published so far (<= M, the row's final max lb); while the workgroup
-//      has more than 32 candidates the running max is read once more (the row's other workgroups
-//      finish their main loops at about the same time and keep publishing);
-//   2. every column of the tile with A_n + E >= M_cur is appended to the row's list (atomicAdd on
-//      the row's count, entry = (order key of A_n + E) << 32 | column).
-// Since M_cur <= M, the lists hold every column k_vrescore would score (every column holding the
-// row's exact maximum passes A_n + E >= L_n >= M); k_vrescore3 keeps the entries whose bound reaches
-// the final M and scores them in exact fp32 (the fma order of k_vocab), so the ids equal
-// k_vscreen2 + k_vrescore's and AA_DECODE_EXACT_VOCAB's bit for bit, in any workgroup order.
-// mk and the counts are [T][B] arrays cleared once per decode; a list longer than LCAP makes its row
-// fall back to every column (correct, slow, never seen).
-// ---------------------------------------------------------------------------------------------
-
-// One transposing butterfly step of a float max over the 32 lanes of a column block (rows kept,
-// as screen_bfly).
-template <int M>
-__device__ __forceinline__ void max_bfly(float (&v)[16], int li) {
-  const bool hi = (li & M) != 0;
-#pragma unroll
-  for (int k = 0; k < M / 2; ++k) {
-    const float s = hi ? v[k] : v[k + M / 2], m = hi ? v[k + M / 2] : v[k];
-    v[k] = fmaxf(m, __uint_as_float(partner<M>(__float_as_uint(s))));
-  }
-}
-
-template <int H>
-__global__ __launch_bounds__(256, 2) void k_vscreen3(int B, int V, int Vp, const bf16x8* __restrict__ ua,
-                                                  const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
-                                                  uint32_t* __restrict__ mk, uint32_t* __restrict__ lcnt,
-                                                  uint64_t* __restrict__ lst, int nread) {
-  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
-  __shared__ float un_s[SC2_BM];
-  __shared__ float m_s[SC2_BM];
-  __shared__ int cnt_s[4];
-  AA_TS(2, 0);
-  const int NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
-  const int L = xcd_remap(blockIdx.x, MT * NT);
-  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 31, lh = lane >> 5;
-  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
-  float bvs[SC2_NB];
-  float2 gsv[SC2_NB];
-#pragma unroll
-  for (int b = 0; b < SC2_NB; ++b) {
-    bvs[b] = bias[n0 + 32 * b + li];
-    gsv[b] = gs[n0 / VS_TILE + b];
-  }
-  floatx16 acc[SC2_NB];
-  screen2_main<H>(B, m0, n0, ua, unorm, wf, Ws, un_s, acc);
-  AA_TS(2, 1);
-  // Bound per element: E = fma(||u||, alpha_g, beta_g) with alpha_g = W_g (CEPS + EPS_ABS) and
-  // beta_g = EPS_ABS B_g (the CEPS bound regrouped; the 1.0001 covers the regrouping's roundings, far
-  // inside CEPS's slack).  Columns past V get the bias -inf: their bounds are -inf (NaN on a garbage
-  // padding row), so they never count.  acc becomes the upper bound A + E.
-  float un16[16], lbm[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    un16[r] = un_s[32 * wave + acc_row(r, lane)];
-    lbm[r] = -INFINITY;
-  }
-#pragma unroll
-  for (int b = 0; b < SC2_NB; ++b) {
-    const float al = gsv[b].x * ((CEPS + EPS_ABS) * 1.0001f), be = gsv[b].y * (EPS_ABS * 1.0001f);
-    const float bv = n0 + 32 * b + li < V ? bvs[b] : -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float E = __builtin_fmaf(un16[r], al, be);
-      const float A = acc[b][r] + bv;
-      lbm[r] = fmaxf(lbm[r], A - E);
-      acc[b][r] = A + E;
-    }
-  }
-  max_bfly<16>(lbm, li);
-  max_bfly<8>(lbm, li);
-  max_bfly<4>(lbm, li);
-  max_bfly<2>(lbm, li);
-  // lane pairs (li, li ^ 1) now hold row rl of the wave's block: publish its lower bound and read the
-  // row's running max back (one atomic round trip)
-  const int rr = (li >> 1) & 15;
-  const int rl = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-  const int prow = m0 + 32 * wave + rl;
-  const bool pub = !(li & 1) && prow < B;
-  uint32_t cur = 0;
-  {
-    const float lb = fmaxf(lbm[0], __uint_as_float(partner<1>(__float_as_uint(lbm[0]))));
-    if (pub) {
-      const uint32_t mine = order_key(lb);
-      cur = atomicMax(mk + (int64_t)prow * MK_LD, mine);
-      cur = cur > mine ? cur : mine;
-    }
-  }
-  AA_TS(2, 2);
-  int reads = 1, tot = 0;
-  for (;;) {
-    if (!(li & 1)) m_s[32 * wave + rl] = prow < B ? key_value(cur) : __builtin_nanf("");  // NaN: no candidates
-    __syncthreads();
-    float M16[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) M16[r] = m_s[32 * wave + acc_row(r, lane)];
-    int n = 0;  // wave-uniform count
-#pragma unroll
-    for (int b = 0; b < SC2_NB; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) n += __popcll(__ballot(acc[b][r] >= M16[r]));  // false on NaN
-    if (lane == 0) cnt_s[wave] = n;
-    __syncthreads();
-    tot = (cnt_s[0] + cnt_s[1]) + (cnt_s[2] + cnt_s[3]);
-    if (tot <= 32 || reads >= nread) {  // uniform over the workgroup: append
-      // compact per wave into LDS entries (order key of the bound << 32 | local row << 8 | local
-      // column) in the dead W stages, then one atomicAdd per candidate, all in flight together,
-      // claims the list slots.  A wave with more than CW candidates (pathological ties) forces the
-      // overflowing rows to k_vrescore3's every-column fallback instead.
-      uint64_t* ent = reinterpret_cast<uint64_t*>(&Ws[0][0]);  // [4][CW]
-      constexpr int CW = (int)(sizeof(Ws) / sizeof(uint64_t) / 4);
-      const uint64_t below = (1ull << lane) - 1ull;
-      int k = 0;
-#pragma unroll
-      for (int b = 0; b < SC2_NB; ++b) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool c = acc[b][r] >= M16[r];
-          const uint64_t mask = __ballot(c);
-          if (__builtin_expect(mask != 0, 0)) {  // wave-uniform: the rare path
-            if (c) {
-              const int i = k + __popcll(mask & below);
-              if (i < CW)
-                ent[wave * CW + i] = ((uint64_t)order_key(acc[b][r]) << 32) | (uint32_t)((acc_row(r, lane) << 8) | (32 * b + li));
-              else
-                atomicAdd(lcnt + (int64_t)(m0 + 32 * wave + acc_row(r, lane)) * LCNT_LD, (uint32_t)LCAP + 1u);
-            }
-            k += __popcll(mask);
-          }
-        }
-      }
-      if (lane == 0) cnt_s[wave] = k < CW ? k : CW;
-      __syncthreads();
-      const int p1 = cnt_s[0], p2 = p1 + cnt_s[1], p3 = p2 + cnt_s[2], nl = p3 + cnt_s[3];
-      for (int i = t; i < nl; i += 256) {
-        const int w = (i >= p1) + (i >= p2) + (i >= p3);
-        const uint64_t e = ent[w * CW + i - (w == 0 ? 0 : w == 1 ? p1 : w == 2 ? p2 : p3)];
-        const int row = m0 + 32 * w + (int)((e >> 8) & 255u), col = n0 + (int)(e & 255u);
-        const uint32_t slot = atomicAdd(lcnt + (int64_t)row * LCNT_LD, 1u);
-        if (slot < (uint32_t)LCAP) lst[(int64_t)row * LCAP + slot] = (e & 0xFFFFFFFF00000000ull) | (uint32_t)col;
-      }
-      break;
-    }
-    ++reads;
-    if (pub) {
-      const uint32_t again = atomicMax(mk + (int64_t)prow * MK_LD, cur);  // = the current max (cur is published)
-      cur = again > cur ? again : cur;
-    }
-    __syncthreads();  // every wave has read m_s / cnt_s before they are rewritten
-  }
-  AA_TS(2, 3);
-  AA_TSV(2, tot + 1000 * reads);
-}
-
-// Rescoring of the lists (greedy path, default): one workgroup per row.  The entries whose bound
-// reaches the row's final M (mk) are the candidates -- every column that can hold the fp32 maximum
-// -- scored 32 per pass in exact fp32 (exact_logit8: k_vocab's fma order); first-index argmax ->
-// keys[row], ids[row, t].  A list that overflowed LCAP falls back to every column.
-template <int H>
-__global__ __launch_bounds__(256) void k_vrescore3(int B, int V, const float* __restrict__ u,
-                                                   const uint32_t* __restrict__ mk, const uint32_t* __restrict__ lcnt,
-                                                   const uint64_t* __restrict__ lst, const float* __restrict__ W,
-                                                   const float* __restrict__ bias, uint64_t* __restrict__ keys,
-                                                   int64_t* __restrict__ ids, int T, int t_step) {
-  __shared__ int cand[LCAP];
-  __shared__ int ncand;
-  __shared__ uint64_t wbest[4];
-  AA_TS(3, 0);
-  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint32_t n = lcnt[(int64_t)row * LCNT_LD];
-  const uint32_t mkey = mk[(int64_t)row * MK_LD];
-  const bool all = n > (uint32_t)LCAP;
-  if (w == 0) {  // one wave compacts the list: keep the entries whose bound reaches M
-    const uint64_t e = lane < (int)n && !all ? lst[(int64_t)row * LCAP + lane] : 0ull;
-    const bool keep = lane < (int)n && !all && (uint32_t)(e >> 32) >= mkey;
-    const uint64_t mask = __ballot(keep);
-    if (keep) cand[__popcll(mask & ((1ull << lane) - 1ull))] = (int)(uint32_t)e;
-    if (lane == 0) ncand = __popcll(mask);
-  }
-  __syncthreads();
-  AA_TS(3, 1);
-  const int nc = all ? V : ncand;
-  const int g = t >> 3, lane8 = t & 7;
-  uint64_t best = 0;
-  for (int i = g; i < nc; i += 32) {
-    const int col = all ? i : cand[i];
-    const float x = exact_logit8<H>(u + (int64_t)row * H, W + (int64_t)col * H, H, bias[col], lane8);
-    const uint64_t k = argmax_key(x, col);
-    best = k > best ? k : best;
-  }
-  best = wave_max_u64(best);
-  if (lane == 0) wbest[w] = best;
-  __syncthreads();
-  if (t == 0) {
-    uint64_t k = wbest[0];
-    for (int i = 1; i < 4; ++i) k = wbest[i] > k ? wbest[i] : k;
-    keys[row] = k;
-    if (ids) ids[(int64_t)row * T + t_step] = key_token(k);
-  }
-  AA_TS(3, 2);
-}
-
 // Exact fp32 logits of selected columns (cols [B][n], -1 = skip) -> out [B][n]; same arithmetic.
 __global__ __launch_bounds__(256) void k_logits_at(int H, int V, const float* __restrict__ u, const int32_t* __restrict__ cols,
                                                    int n, const float* __restrict__ W, const float* __restrict__ bias,
@@ -3082,11 +2477,11 @@ static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
 // features, and `s` waits for aux before returning.
 // the encoder's V GEMM runs on k_enc_v4 (which also writes the compressed V when asked)
 static bool enc_v4(const Layout& L, int32_t flags) {
-  return !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && (L.H == 512 || L.H == 256) && L.C <= E4_MAXC;
+  return !(flags & AA_DECODE_FP32_ENCODER) && (L.H == 512 || L.H == 256) && L.C <= E4_MAXC;
 }
 // x_g and VWv on k_gemm3 (bf16x3) unless an fp32-MFMA encoder was asked for; K % 256 == 0 (4 waves)
 static bool gemm3_ok(int32_t flags, int K) {
-  return !(flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER)) && K % 256 == 0;
+  return !(flags & AA_DECODE_FP32_ENCODER) && K % 256 == 0;
 }
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
@@ -3105,7 +2500,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
   auto heads_xg = [&](hipStream_t st) {
     rec(ev, 4, st);
     const int NH = E + 2 * H;
-    if (flags & (AA_DECODE_ENC_V3 | AA_DECODE_FP32_ENCODER) || C % 256) {
+    if (flags & AA_DECODE_FP32_ENCODER || C % 256) {
       const int MT = (B + 63) / 64, NTn = L.NHp / 64;
       hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
                          v_g, h0, c0);
@@ -3228,13 +2623,11 @@ static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
 }
 
 struct DecodeWS {
-  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part, *gates;
+  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part;
   uint16_t* ub;
   bf16x8* hsp[2];
   float4* summ;
   uint64_t* keys;
-  uint32_t *mk, *lcnt;  // [T][B] running max lower bound and candidate count per row (k_vscreen3)
-  uint64_t* lst;        // [T][B][LCAP] candidate lists (k_vscreen3 -> k_vrescore3)
   int64_t* tok0;
 };
 static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* bytes) {
@@ -3253,14 +2646,10 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   w.u = c.take<float>((size_t)B * L.H);
   w.unorm = c.take<float>((size_t)B);
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
-  w.gates = c.take<float>((size_t)B * 4 * L.H);  // split LSTM step: h W_hh^T of the next step
   w.ub = c.take<uint16_t>((size_t)((B + 127) / 128) * 128 * L.H);  // fragment order, 128-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
   w.keys = c.take<uint64_t>((size_t)T * B);
-  w.mk = c.take<uint32_t>((size_t)T * B * MK_LD);
-  w.lcnt = c.take<uint32_t>((size_t)T * B * LCNT_LD);
-  w.lst = c.take<uint64_t>((size_t)T * B * LCAP);
   w.tok0 = c.take<int64_t>((size_t)B);
   *bytes = c.off;
   return w;
@@ -3303,40 +2692,6 @@ static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok,
     default: AA_LSTM(1024); break;
   }
 #undef AA_LSTM
-}
-
-// Split LSTM step, part 1 (k_lstm_gemm): gates = h_{t-1} W_hh^T for all B rows.
-static void lstm_gemm_launch(const Layout& L, const MP& p, int B, const bf16x8* hsp_in, float* gates, hipStream_t s) {
-  const int H = L.H, MT = (B + 63) / 64;
-  switch (H) {
-    case 256: hipLaunchKernelGGL(k_lstm_gemm<256>, dim3(MT * 16), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
-    case 512: hipLaunchKernelGGL(k_lstm_gemm<512>, dim3(MT * 32), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
-    case 768: hipLaunchKernelGGL(k_lstm_gemm<768>, dim3(MT * 48), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
-    default: hipLaunchKernelGGL(k_lstm_gemm<1024>, dim3(MT * 64), dim3(512), 0, s, B, hsp_in, p.whh3, gates); break;
-  }
-}
-
-// Split LSTM step, part 2 (k_lstm_cell): the cell on the gates of part 1.
-static void lstm_cell_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
-                             const float* gates, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
-                             float* s_buf, float* part, hipStream_t s, const int* par = nullptr) {
-  const int H = L.H, MT = (B + 63) / 64;
-#define AA_CELL(H_)                                                                                           \
-  do {                                                                                                        \
-    if (par)                                                                                                  \
-      hipLaunchKernelGGL((k_lstm_cell<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, gates, c_in, par, p.wgs, h_out, hsp_out, c_out, s_buf, part);          \
-    else                                                                                                      \
-      hipLaunchKernelGGL((k_lstm_cell<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, gates, c_in, par, p.wgs, h_out, hsp_out, c_out, s_buf, part);          \
-  } while (0)
-  switch (H) {
-    case 256: AA_CELL(256); break;
-    case 512: AA_CELL(512); break;
-    case 768: AA_CELL(768); break;
-    default: AA_CELL(1024); break;
-  }
-#undef AA_CELL
 }
 
 // Attention for one step (kdiv rows per image: beam search; k_atten5b runs an image's rows together)
@@ -3431,270 +2786,116 @@ int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const
   return launch_status();
 }
 
-// wide vocab-screen tiles (k_vscreen2 / k_vscreen3) when the padded vocabulary is whole 160-column
-// tiles (V = 10,123: 64 of them) and a wave's u fragments fit its registers
-static bool screen_wide(const Layout& L, int32_t flags) {
-  return L.Vp % SC2_BN == 0 && L.H <= 512 && !(flags & AA_DECODE_SCREEN64);
-}
-// the greedy decode's opt-in vocab stage: k_vscreen3 (screen + candidate lists) + k_vrescore3
-static bool greedy_lists(const Layout& L, int32_t flags) {
-  return (flags & AA_DECODE_LISTS) && !(flags & AA_DECODE_EXACT_VOCAB) && screen_wide(L, flags);
-}
+// wide vocab-screen tiles (k_vscreen2) when the padded vocabulary is whole 160-column tiles
+// (V = 10,123: 64 of them) and a wave's u fragments fit its registers; k_vscreen otherwise
+static bool screen_wide(const Layout& L) { return L.Vp % SC2_BN == 0 && L.H <= 512; }
 
-// reads of the running lower bound per row in k_vscreen3 (AA_SR_READS: tuning experiments)
-static int sr_reads() {
-  static int n = [] {
-    const char* e = getenv("AA_SR_READS");
-    const int v = e ? atoi(e) : 2;
-    return v < 1 ? 1 : (v > 8 ? 8 : v);
-  }();
-  return n;
-}
-
-// The T-step loop over rows [r0, r0 + Bl) of the batch (every workspace array is row-indexed, so a
-// lane is the same loop on offset pointers; keys are [T][B]).
-// sg != nullptr: split LSTM steps -- k_lstm_gemm for step t+1 (it needs only h_t) runs on sg beside
-// step t's attention, vocab screen and rescoring on s, and k_lstm_cell of step t+1 waits for it
-// (sg == s: the same kernels in stream order).  sg == nullptr: the fused k_lstm.
-static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int r0, int Bl, int T, int32_t flags,
-                       int64_t* ids, float* alpha, float* beta, const aa_trace* trace, hipStream_t s,
-                       hipStream_t sg = nullptr) {
+// The T-step loop over the B rows: k_lstm (GEMM + cell + attention projections), k_atten, then the
+// vocab stage -- k_vscreen2 (bf16 screen, granule summaries) + k_vrescore (exact fp32 rescoring of
+// the candidates), or with AA_DECODE_EXACT_VOCAB the exact fp32 GEMM k_vocab + k_key_ids.
+static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int T, int32_t flags, int64_t* ids,
+                       float* alpha, float* beta, const aa_trace* trace, hipStream_t s) {
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
-  const int H = L.H, MT = (Bl + 63) / 64, NTn = L.Vp / VS_TILE;
-  const bool wide = screen_wide(L, flags);
-  // AA_DECODE_LISTS: the screen writes per-row candidate lists (k_vscreen3), rescored by k_vrescore3
-  const bool lists = greedy_lists(L, flags);
-  const float* V = w.V + (size_t)r0 * P * H;
-  const float* vwv = w.vwv + (size_t)r0 * P * PP;
-  const float* xg = w.xg + (size_t)r0 * L.N5;
-  float* hb[2] = {w.h[0] + (size_t)r0 * H, w.h[1] + (size_t)r0 * H};
-  const size_t fo = (size_t)(r0 / 32) * (H / 16) * 3 * 64;  // r0 is a multiple of 64
-  bf16x8* hs[2] = {w.hsp[0] + fo, w.hsp[1] + fo};
-  float* cb[2] = {w.c[0] + (size_t)r0 * H, w.c[1] + (size_t)r0 * H};
-  float* sb = w.s + (size_t)r0 * H;
-  float* part = w.part + (size_t)r0 * (H / 16) * PART;
-  float* u = w.u + (size_t)r0 * H;
-  uint16_t* ub = w.ub + (size_t)r0 * H;
-  float* unorm = w.unorm + r0;
-  float4* summ = w.summ + (size_t)r0 * NTn;
-  int64_t* idsl = ids + (size_t)r0 * T;
-  float* al = alpha ? alpha + (size_t)r0 * T * P : nullptr;
-  float* bl = beta ? beta + (size_t)r0 * T : nullptr;
-  float* gates = w.gates + (size_t)r0 * 4 * H;
-  const bool split = sg != nullptr, two = split && sg != s;
-  aa_event_t* gev = trace ? trace->gemm_events : nullptr;
-  aa_event_t* lev = trace ? trace->lstm_events : nullptr;
-  aa_event_t* aev = trace ? trace->atten_events : nullptr;
-  hipEvent_t ev_h = nullptr, ev_g = nullptr;  // h_t ready (s -> sg), gates ready (sg -> s)
-  auto gemm = [&](int t, hipStream_t gs) {   // gates of step t from h_{t-1} (fragments hs[t & 1])
-    rec(gev, 2 * t, gs);
-    lstm_gemm_launch(L, p, Bl, hs[t & 1], gates, gs);
-    rec(gev, 2 * t + 1, gs);
-  };
-  if (two) {
-    AA_TRY(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
-    AA_TRY(hipEventCreateWithFlags(&ev_g, hipEventDisableTiming));
-    AA_TRY(hipEventRecord(ev_h, s));
-    AA_TRY(hipStreamWaitEvent(sg, ev_h, 0));
-  }
-  if (split) {
-    gemm(0, sg);
-    if (two) AA_TRY(hipEventRecord(ev_g, sg));
-  }
+  const int H = L.H, MT = (B + 63) / 64;
+  const bool wide = screen_wide(L);
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
-    // token of step t-1: ids[:, t-1] (written by the previous step) or, fused, the argmax keys of
-    // step t-1; <start> at t = 0
     // token of step t-1: ids[:, t-1] (written by the previous step), <start> at t = 0
-    const int64_t* tok = t ? idsl + (t - 1) : w.tok0 + r0;
+    const int64_t* tok = t ? ids + (t - 1) : w.tok0;
     const int tok_ld = t ? T : 1;
-    uint64_t* kt = w.keys + (size_t)t * B + r0;
-    float* alt = al ? al + (size_t)t * P : nullptr;
-    float* blt = bl ? bl + t : nullptr;
-    if (split) {
-      if (two) AA_TRY(hipStreamWaitEvent(s, ev_g, 0));
-      rec(lev, 2 * t, s);
-      lstm_cell_launch(L, p, Bl, tok, tok_ld, xg, gates, cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, s);
-      rec(lev, 2 * t + 1, s);
-      if (two && t + 1 < T) {
-        AA_TRY(hipEventRecord(ev_h, s));
-        AA_TRY(hipStreamWaitEvent(sg, ev_h, 0));
-        gemm(t + 1, sg);
-        AA_TRY(hipEventRecord(ev_g, sg));
-      }
-      rec(aev, 2 * t, s);
-      atten_launch(L, p, Bl, V, vwv, hb[nxt], sb, part, u, exact ? nullptr : ub, exact ? nullptr : unorm, alt,
-                   (int64_t)T * P, blt, T, s);
-      rec(aev, 2 * t + 1, s);
-    } else {
-      lstm_atten_launch(L, p, Bl, tok, tok_ld, V, vwv, xg, hs[cur], cb[cur], hb[nxt], hs[nxt], cb[nxt], sb, part, u,
-                        exact ? nullptr : ub, exact ? nullptr : unorm, alt, (int64_t)T * P, blt, T, trace, t, s,
-                        nullptr, 1, nullptr);
-    }
+    uint64_t* kt = w.keys + (size_t)t * B;
+    float* alt = alpha ? alpha + (size_t)t * P : nullptr;
+    float* blt = beta ? beta + t : nullptr;
+    lstm_atten_launch(L, p, B, tok, tok_ld, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt], w.c[nxt],
+                      w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm, alt, (int64_t)T * P, blt,
+                      T, trace, t, s, nullptr, 1, nullptr);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     rec(sev, 2 * t, s);
     if (exact) {
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, Bl, L.H, L.V, L.Vp, L.V, u, p.mlp_w, p.mlp_b,
-                         nullptr, kt);
+      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V, w.u, p.mlp_w,
+                         p.mlp_b, nullptr, kt);
       rec(sev, 2 * t + 1, s);
-      hipLaunchKernelGGL(k_key_ids, dim3((Bl + 255) / 256), dim3(256), 0, s, kt, Bl, idsl + t, T);
-    } else {
-#define AA_SCREEN(H_)                                                                                    \
-  hipLaunchKernelGGL(k_vscreen<H_>, dim3(((Bl + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, Bl, L.V, \
-                     L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                        \
-                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
-#define AA_SCREEN2(H_)                                                                                      \
-  hipLaunchKernelGGL((AA_SCREEN_DMA && H_ == 512 ? k_vscreen4<H_> : k_vscreen2<H_>),                          \
-                     dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl,                 \
-                     L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
-                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, summ)
-#define AA_SCREEN3(H_)                                                                                      \
-  hipLaunchKernelGGL(k_vscreen3<H_>, dim3(((Bl + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, Bl, \
-                     L.V, L.Vp, reinterpret_cast<const bf16x8*>(ub), unorm,                                    \
-                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, mkt, lct, lst, sr_reads())
-#define AA_RESCORE3(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vrescore3<H_>, dim3(Bl), dim3(256), 0, s, Bl, L.V, u, mkt, lct, lst, p.mlp_w, p.mlp_b, kt, \
-                     idsl, T, t)
-      if (lists) {
-        uint32_t* mkt = w.mk + ((size_t)t * B + r0) * MK_LD;
-        uint32_t* lct = w.lcnt + ((size_t)t * B + r0) * LCNT_LD;
-        uint64_t* lst = w.lst + ((size_t)t * B + r0) * LCAP;
-        if (H == 256) AA_SCREEN3(256);
-        else AA_SCREEN3(512);
-        rec(sev, 2 * t + 1, s);
-        rec(rev, 2 * t, s);
-        if (H == 256) AA_RESCORE3(256);
-        else AA_RESCORE3(512);
-        rec(rev, 2 * t + 1, s);
-      } else {
-        switch (H) {
-          case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
-          case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
-          case 768: AA_SCREEN(768); break;
-          default: AA_SCREEN(1024); break;
-        }
-        rec(sev, 2 * t + 1, s);
-        rec(rev, 2 * t, s);
+      hipLaunchKernelGGL(k_key_ids, dim3((B + 255) / 256), dim3(256), 0, s, kt, B, ids + t, T);
+      continue;
+    }
+#define AA_SCREEN(H_)                                                                                          \
+  hipLaunchKernelGGL(k_vscreen<H_>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V, L.Vp, \
+                     reinterpret_cast<const bf16x8*>(w.ub), w.unorm, reinterpret_cast<const bf16x8*>(p.mlp_wb),  \
+                     p.mlp_gs, p.mlp_b, w.summ)
+#define AA_SCREEN2(H_)                                                                                          \
+  hipLaunchKernelGGL(k_vscreen2<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, B, L.V, \
+                     L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,                                          \
+                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
 #define AA_RESCORE(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vrescore<H_>, dim3(Bl), dim3(RS_NT), 0, s, Bl, L.V, L.Vp, u, summ, p.mlp_w, p.mlp_b, kt, idsl, T, t)
-        switch (H) {
-          case 256: AA_RESCORE(256); break;
-          case 512: AA_RESCORE(512); break;
-          case 768: AA_RESCORE(768); break;
-          default: AA_RESCORE(1024); break;
-        }
-#undef AA_RESCORE
-        rec(rev, 2 * t + 1, s);
-      }
+  hipLaunchKernelGGL(k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt, \
+                     ids, T, t)
+    switch (H) {
+      case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
+      case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
+      case 768: AA_SCREEN(768); break;
+      default: AA_SCREEN(1024); break;
+    }
+    rec(sev, 2 * t + 1, s);
+    rec(rev, 2 * t, s);
+    switch (H) {
+      case 256: AA_RESCORE(256); break;
+      case 512: AA_RESCORE(512); break;
+      case 768: AA_RESCORE(768); break;
+      default: AA_RESCORE(1024); break;
+    }
+    rec(rev, 2 * t + 1, s);
 #undef AA_SCREEN
 #undef AA_SCREEN2
-#undef AA_SCREEN3
-#undef AA_RESCORE3
-    }
-    if (split && !two && t + 1 < T) gemm(t + 1, s);
-  }
-  if (two) {  // every sg launch was waited for by a k_lstm_cell on s
-    AA_TRY(hipEventDestroy(ev_h));
-    AA_TRY(hipEventDestroy(ev_g));
+#undef AA_RESCORE
   }
   return launch_status();
 }
 
+// aux: optional second stream for the encoder's a_g branch (heads -> x_g beside the VWv GEMM);
+// `s` waits for it before the step loop.
 static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
                        float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
-                       hipStream_t s, const aa_stream_t* lanes, int32_t n_lanes, hipStream_t aux = nullptr) {
+                       hipStream_t s, hipStream_t aux = nullptr) {
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
-  if (B < 0 || T < 0 || n_lanes < 0) return AA_ERR_SHAPE;
+  if (B < 0 || T < 0) return AA_ERR_SHAPE;
   if (B == 0 || T == 0) return AA_OK;
-  if (!feats || !ids || !workspace || (n_lanes > 0 && !lanes)) return AA_ERR_NULL;
+  if (!feats || !ids || !workspace) return AA_ERR_NULL;
   if (!al16(feats) || !al16(workspace)) return AA_ERR_ALIGN;
   size_t need;
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
-  // lanes: contiguous row ranges, whole 64-row tiles where possible, each decoded on its own stream
-  int nl = n_lanes > 0 ? n_lanes : 1;
-  const int tiles = (B + 63) / 64;
-  if (nl > tiles) nl = tiles;
-  if (nl > AA_MAX_LANES) nl = AA_MAX_LANES;
-  if (!aux && n_lanes > 1) aux = (hipStream_t)lanes[1];
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, flags, s, aux);
   if (rc) return rc;
   hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
                      L.H, w.hsp[0]);
   {
-    // atomics accumulate into keys (k_vocab) and, for the lists, mk / lcnt; the default vocab stage
-    // writes every key it produces, so it needs no clearing
-    const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0, lists = greedy_lists(L, flags);
-    const int n = exact || lists ? T * B : 0, nb = n > B ? n : B;
+    // the exact vocab stage accumulates into keys by atomicMax (k_vocab); the default stage writes
+    // every key it produces, so it needs no clearing
+    const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
+    const int n = exact ? T * B : 0, nb = n > B ? n : B;
     const int nblk = nb / 256 + 1;
     hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1,
-                       exact ? w.keys : nullptr, lists ? w.mk : nullptr, lists ? w.lcnt : nullptr, n);
+                       exact ? w.keys : nullptr, n);
   }
-  if (nl == 1) {
-    hipStream_t ls = n_lanes > 0 ? (hipStream_t)lanes[0] : s;
-    hipEvent_t e = nullptr;
-    if (ls != s) {
-      AA_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      AA_TRY(hipEventRecord(e, s));
-      AA_TRY(hipStreamWaitEvent(ls, e, 0));
-    }
-    // the split LSTM step uses the aux stream (if any) for the GEMM of the next step
-    hipStream_t sg = (flags & AA_DECODE_FUSED_LSTM) || !aux || aux == ls ? nullptr : aux;
-    rc = decode_rows(L, p, w, B, 0, B, T, flags, ids, alpha, beta, trace, ls, sg);
-    if (rc) return rc;
-    if (ls != s) {
-      AA_TRY(hipEventRecord(e, ls));
-      AA_TRY(hipStreamWaitEvent(s, e, 0));
-      AA_TRY(hipEventDestroy(e));
-    }
-  } else {
-    hipEvent_t fork, join[AA_MAX_LANES];
-    AA_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-    AA_TRY(hipEventRecord(fork, s));
-    for (int i = 0; i < nl; ++i) {
-      const int r0 = (int)((int64_t)tiles * i / nl) * 64;
-      int r1 = (int)((int64_t)tiles * (i + 1) / nl) * 64;
-      if (r1 > B) r1 = B;
-      hipStream_t ls = (hipStream_t)lanes[i];
-      AA_TRY(hipStreamWaitEvent(ls, fork, 0));
-      rc = decode_rows(L, p, w, B, r0, r1 - r0, T, flags, ids, alpha, beta, i == 0 ? trace : nullptr, ls);
-      if (rc) return rc;
-      AA_TRY(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
-      AA_TRY(hipEventRecord(join[i], ls));
-    }
-    for (int i = 0; i < nl; ++i) {
-      AA_TRY(hipStreamWaitEvent(s, join[i], 0));
-      AA_TRY(hipEventDestroy(join[i]));
-    }
-    AA_TRY(hipEventDestroy(fork));
-  }
-  return launch_status();
+  return decode_rows(L, p, w, B, T, flags, ids, alpha, beta, trace, s);
 }
 
 int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
                      float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                      aa_stream_t stream) {
-  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
-                     nullptr, 0);
+  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream);
 }
 
 int aa_greedy_decode_aux(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
                          float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                          aa_stream_t stream, aa_stream_t aux_stream) {
   return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
-                     nullptr, 0, (hipStream_t)aux_stream);
-}
-
-int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
-                           float* beta, void* workspace, size_t workspace_bytes, const aa_trace* trace, int32_t flags,
-                           aa_stream_t stream, const aa_stream_t* lanes, int32_t n_lanes) {
-  return greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, trace, flags, (hipStream_t)stream,
-                     lanes, n_lanes);
+                     (hipStream_t)aux_stream);
 }
 
 // ---- decode plans: the whole greedy decode captured once into a hipGraph ------------------------
@@ -3702,30 +2903,25 @@ struct aa_decode_plan {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipStream_t cap = nullptr, aux = nullptr;
-  hipStream_t lanes[AA_MAX_LANES] = {};
-  int n_lanes = 0;
 };
 
 static void plan_free(aa_decode_plan* p) {
   if (!p) return;
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
-  for (int i = 0; i < p->n_lanes; ++i)
-    if (p->lanes[i]) (void)hipStreamDestroy(p->lanes[i]);
   if (p->cap) (void)hipStreamDestroy(p->cap);
   if (p->aux) (void)hipStreamDestroy(p->aux);
   delete p;
 }
 
 int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,
-                          float* beta, void* workspace, size_t workspace_bytes, int32_t flags, int32_t n_lanes,
-                          aa_decode_plan** out) {
+                          float* beta, void* workspace, size_t workspace_bytes, int32_t flags, aa_decode_plan** out) {
   if (!out) return AA_ERR_NULL;
   *out = nullptr;
   Layout L;
   int rc = check_model(m, &L);
   if (rc) return rc;
-  if (B <= 0 || T <= 0 || n_lanes < 0 || n_lanes > AA_MAX_LANES) return AA_ERR_SHAPE;
+  if (B <= 0 || T <= 0) return AA_ERR_SHAPE;
   if (!feats || !ids || !workspace) return AA_ERR_NULL;
   if (!al16(feats) || !al16(workspace)) return AA_ERR_ALIGN;
   size_t need;
@@ -3734,18 +2930,12 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
   aa_decode_plan* p = new aa_decode_plan();
   hipError_t e = hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking);
-  const int nl = n_lanes > 1 ? n_lanes : 0;
-  for (int i = 0; e == hipSuccess && i < nl; ++i) {
-    e = hipStreamCreateWithFlags(&p->lanes[i], hipStreamNonBlocking);
-    if (e == hipSuccess) p->n_lanes = i + 1;
-  }
   if (e == hipSuccess) e = hipStreamBeginCapture(p->cap, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {
     plan_free(p);
     return (int)e;
   }
   rc = greedy_impl(m, feats, B, T, ids, alpha, beta, workspace, workspace_bytes, nullptr, flags, p->cap,
-                   reinterpret_cast<const aa_stream_t*>(p->lanes), nl,
                    (flags & AA_DECODE_ONE_STREAM) ? nullptr : p->aux);
   e = hipStreamEndCapture(p->cap, &p->graph);
   if (rc == 0 && e != hipSuccess) rc = (int)e;
@@ -3762,10 +2952,6 @@ int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int3
   (void)hipStreamDestroy(p->cap);
   (void)hipStreamDestroy(p->aux);
   p->cap = p->aux = nullptr;
-  for (int i = 0; i < p->n_lanes; ++i) {
-    (void)hipStreamDestroy(p->lanes[i]);
-    p->lanes[i] = nullptr;
-  }
   *out = p;
   return AA_OK;
 }

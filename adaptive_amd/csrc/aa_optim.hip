@@ -13,6 +13,28 @@
 
 namespace aa_optim {
 
+__global__ __launch_bounds__(256) void k_read_probe(const float4* __restrict__ src, int64_t n, float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  float acc = 0.f;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 7 * stride < n; i += 8 * stride) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+  }
+  for (; i < n; i += stride) {
+    const float4 v = src[i];
+    acc += (v.x + v.y) + (v.z + v.w);
+  }
+  __shared__ float red[4];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // ---- Adam (torch.optim.Adam, amsgrad=False, maximize=False; model_factory.py:71 builds it) -------------
 // One workgroup = ADAM_CHUNK consecutive elements of one tensor.  The per-tensor table travels in
 // the kernel arguments (no upload, no allocation).
@@ -258,14 +280,15 @@ __global__ __launch_bounds__(1024) void k_ce_reduce(const float* __restrict__ lo
   }
 }
 
-__global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* __restrict__ x, int64_t ldx, int V,
+// x and dx may alias (dlogits in place of logits, lddx == ldx): every element is read by the thread
+// that writes it, before the write, so neither pointer is __restrict__
+__global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* x, int64_t ldx, int V,
                                                        const int64_t* __restrict__ tgt, int64_t ignore,
                                                        const float* __restrict__ lse, const float* __restrict__ dloss,
-                                                       const float* __restrict__ count, float* __restrict__ dx,
-                                                       int64_t lddx) {
+                                                       const float* __restrict__ count, float* dx, int64_t lddx) {
   const int row = blockIdx.x;
-  const float* __restrict__ xr = x + (int64_t)row * ldx;
-  float* __restrict__ dr = dx + (int64_t)row * lddx;
+  const float* xr = x + (int64_t)row * ldx;
+  float* dr = dx + (int64_t)row * lddx;
   const int64_t t = tgt[row];
   const float scale = (t == ignore) ? 0.f : dloss[0] / count[0];
   const float L = lse[row];
@@ -360,11 +383,27 @@ int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, int64_t 
 
 int aa_cross_entropy_backward(const float* logits, int32_t N, int32_t V, int64_t ldx, const int64_t* targets,
                               int64_t ignore_index, const float* dloss, const float* count, const void* workspace,
-                              float* dlogits, int64_t lddx, aa_stream_t stream) {
+                              size_t workspace_bytes, float* dlogits, int64_t lddx, aa_stream_t stream) {
   if (N <= 0 || V <= 0 || ldx < V || lddx < V) return AA_ERR_SHAPE;
   if (!logits || !targets || !dloss || !count || !workspace || !dlogits) return AA_ERR_NULL;
+  // the forward's per-row log-sum-exp: a workspace from a forward over fewer rows is refused
+  if (workspace_bytes < aa_cross_entropy_workspace_bytes(N)) return AA_ERR_BUFFER;
+  if (dlogits == logits && lddx != ldx) return AA_ERR_SHAPE;  // in place only with the same pitch
   hipLaunchKernelGGL(k_ce_bwd, dim3(N), dim3(CE_THREADS), 0, (hipStream_t)stream, logits, ldx, V, targets,
                      ignore_index, (const float*)workspace, dloss, count, dlogits, lddx);
+  return (int)hipGetLastError();
+}
+
+// Measurement helper (bench.py): one streaming read of [src, src + nbytes) by 16-B loads, grid-stride,
+// 8 loads in flight per thread, each workgroup's sum written to out[blockIdx.x] (so the loads are not
+// dead).  Read twice over a buffer that fits the 256 MiB Infinity Cache, the second pass measures the
+// MALL-served read rate that k_atten's per-step re-read of V (51.4 MB at B = 512) runs against; over a
+// buffer several times that size, the HBM read rate.
+int aa_read_probe(const void* src, size_t nbytes, float* out, int32_t blocks, aa_stream_t stream) {
+  if (!src || !out) return AA_ERR_NULL;
+  if (blocks <= 0 || nbytes % 16 || ((uintptr_t)src & 15)) return AA_ERR_SHAPE;
+  hipLaunchKernelGGL(aa_optim::k_read_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const float4*>(src), (int64_t)(nbytes / 16), out);
   return (int)hipGetLastError();
 }
 

@@ -1145,7 +1145,8 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
     w.ub = c.take<__bf16>(R * H);
     w.wmb = c.take<__bf16>((size_t)d.vocab * H);
     w.dspb = c.take<__bf16>(R * Kv);
-    w.wmT = c.take<__bf16>(H * Kv);
+    // W_m^T [H][Kv] in the backward; the bf16 forward's encoder also packs W_a [H][C] here
+    w.wmT = c.take<__bf16>(H * (Kv > Cc ? Kv : Cc));
     w.dspT = c.take<__bf16>((size_t)d.vocab * Kr);
     w.upT = c.take<__bf16>(H * Kr);
     w.dvT = c.take<__bf16>(H * Kb);

@@ -20,30 +20,44 @@ def hip() -> ctypes.CDLL:
         lib = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
         lib.hipEventCreate.argtypes = [POINTER(c_void_p)]
         lib.hipEventCreate.restype = c_int
+        lib.hipEventCreateWithFlags.argtypes = [POINTER(c_void_p), ctypes.c_uint]
+        lib.hipEventCreateWithFlags.restype = c_int
         lib.hipEventDestroy.argtypes = [c_void_p]
         lib.hipEventDestroy.restype = c_int
         lib.hipEventElapsedTime.argtypes = [POINTER(c_float), c_void_p, c_void_p]
         lib.hipEventElapsedTime.restype = c_int
         lib.hipEventSynchronize.argtypes = [c_void_p]
         lib.hipEventSynchronize.restype = c_int
+        lib.hipEventRecord.argtypes = [c_void_p, c_void_p]
+        lib.hipEventRecord.restype = c_int
         lib.hipStreamCreateWithFlags.argtypes = [POINTER(c_void_p), ctypes.c_uint]
         lib.hipStreamCreateWithFlags.restype = c_int
         lib.hipStreamDestroy.argtypes = [c_void_p]
         lib.hipStreamDestroy.restype = c_int
+        lib.hipMemcpyAsync.argtypes = [c_void_p, c_void_p, ctypes.c_size_t, c_int, c_void_p]
+        lib.hipMemcpyAsync.restype = c_int
         _hip = lib
     return _hip
 
 
-class EventArray:
-    """n raw hipEvent_t handles as a C array (pass ``.ptr`` as an ``aa_event_t*``)."""
+# hipEventDisableSystemFence | hipEventReleaseToDevice: timing-only events -- no system-scope fence
+# (cache writeback / invalidate) when the event is recorded, a device-scope release instead, so the
+# kernels between two events are timed without the fence's cost (hip_runtime_api.h)
+TIMING_FLAGS = 0x20000000 | 0x40000000
 
-    def __init__(self, n: int):
+
+class EventArray:
+    """n raw hipEvent_t handles as a C array (pass ``.ptr`` as an ``aa_event_t*``).  ``precise``:
+    timing-only events (TIMING_FLAGS), the default for per-kernel timing."""
+
+    def __init__(self, n: int, precise: bool = True):
         self.n = n
         self.arr = (c_void_p * n)()
         h = hip()
         for i in range(n):
             ev = c_void_p()
-            rc = h.hipEventCreate(ctypes.byref(ev))
+            rc = (h.hipEventCreateWithFlags(ctypes.byref(ev), TIMING_FLAGS) if precise
+                  else h.hipEventCreate(ctypes.byref(ev)))
             if rc != 0:
                 raise RuntimeError(f"hipEventCreate failed: {rc}")
             self.arr[i] = ev.value
@@ -60,6 +74,12 @@ class EventArray:
         if rc != 0:
             raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
         return ms.value
+
+    def record(self, i: int, stream) -> None:
+        """Record event i on ``stream`` (a torch stream)."""
+        rc = hip().hipEventRecord(self.arr[i], stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed: {rc}")
 
     def pair_durations_ms(self, npairs: int | None = None):
         npairs = self.n // 2 if npairs is None else npairs
@@ -80,7 +100,7 @@ class EventArray:
 
 
 _raw_streams = {}
-_owned_streams = []  # streams handed out by new_raw_stream (kept alive for the process)
+_role_streams = {}  # (device index, role) -> stream: a bounded pool, one stream per role and device
 
 
 def _create(idx: int) -> "torch.cuda.ExternalStream":
@@ -112,10 +132,34 @@ def raw_streams(device, n: int):
     return have[:n]
 
 
-def new_raw_stream(device) -> "torch.cuda.ExternalStream":
-    """A fresh non-blocking HIP stream on ``device`` that no other caller of this module gets (it
-    takes the next hardware queue in HIP's round-robin at the time of the call).  Kept alive for the
-    process, as ``raw_streams``."""
-    st = _create(_index(device))
-    _owned_streams.append(st)
+def role_stream(device, role: str) -> "torch.cuda.ExternalStream":
+    """The process's fresh non-blocking HIP stream for ``role`` on ``device`` (created on first use,
+    then shared by every caller asking for the same role: e.g. the decode's aux stream, or a
+    device-parallel shard stream).  The pool is bounded by the roles in use, so building models or
+    pipelines in a loop creates no further streams.  Each new role's stream takes the next hardware
+    queue in HIP's round-robin; like ``raw_streams`` they live as long as the process (torch's caching
+    allocator may still record events on them)."""
+    key = (_index(device), str(role))
+    st = _role_streams.get(key)
+    if st is None:
+        st = _role_streams[key] = _create(key[0])
     return st
+
+
+HIP_MEMCPY_DEFAULT = 4  # hipMemcpyDefault: direction from the pointers (unified addressing)
+
+
+def copy_async(dst: "torch.Tensor", src: "torch.Tensor", stream) -> None:
+    """dst <- src (contiguous, same shape and dtype, on any devices) by one hipMemcpyAsync queued on
+    ``stream`` and on that stream ONLY.  torch's cross-device ``copy_`` instead synchronises the
+    current streams of both devices around the copy (ATen's device-to-device copy), which would
+    serialise the devices of a single-process multi-device decode; the caller orders this copy with
+    events instead."""
+    if dst.shape != src.shape or dst.dtype != src.dtype or not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("copy_async: dst and src must be contiguous tensors of one shape and dtype")
+    n = src.numel() * src.element_size()
+    if n == 0:
+        return
+    rc = hip().hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), n, HIP_MEMCPY_DEFAULT, stream.cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed: {rc}")

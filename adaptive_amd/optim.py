@@ -57,15 +57,20 @@ class Adam(torch.optim.Optimizer):
         lib = _lib.load()
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
-            by_step = {}  # tensors that share a step count go in one call
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            # validate every parameter of the group first: a rejected tensor must leave no parameter
+            # with a step count for an update that never ran (torch's bias correction would drift)
+            live = [p for p in group["params"] if p.grad is not None]
+            for p in live:
                 if p.grad.is_sparse:
                     raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
                 _require_hip(p, "parameter")
+                _require_hip(p.grad, "gradient")
                 if not (p.is_contiguous() and p.grad.is_contiguous()):
                     raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
+                if p.grad.shape != p.shape or p.grad.device != p.device:
+                    raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
+            by_step = {}  # tensors that share a step count go in one call
+            for p in live:
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
@@ -117,8 +122,8 @@ class _CrossEntropy(torch.autograd.Function):
         dx = torch.empty(N, V, dtype=torch.float32, device=x.device)
         with torch.cuda.device(x.device):
             rc = lib.aa_cross_entropy_backward(x.data_ptr(), N, V, x.stride(0), target.data_ptr(), ctx.ignore_index,
-                                               dloss.data_ptr(), count.data_ptr(), ws.data_ptr(), dx.data_ptr(),
-                                               dx.stride(0), _lib.stream_handle())
+                                               dloss.data_ptr(), count.data_ptr(), ws.data_ptr(), ws.numel(),
+                                               dx.data_ptr(), dx.stride(0), _lib.stream_handle())
         _lib.check(rc, "cross_entropy_backward")
         return dx, None, None
 

@@ -6,8 +6,8 @@ One B = 512 decode is latency-bound on MI355X: its step kernels hold one or two 
 and the encoder GEMM cannot start before the previous batch's last step.  Batches are independent,
 so batch i + 1 (encoder and first steps) runs on a second stream while batch i finishes: same
 kernels, same per-batch work and the same ids bit for bit (tests/test_gpu_parity.py), more of the
-chip busy.  Each slot owns its stream, workspace (or captured decode plan) and output buffers; the
-caller's stream waits for a batch's completion event only when that batch's result is handed out.
+chip busy.  Each slot owns its stream, workspace and output buffers; the caller's stream waits for a
+batch's completion event only when that batch's result is handed out.
 """
 from __future__ import annotations
 
@@ -17,26 +17,14 @@ from typing import Iterable, Iterator, Tuple
 import torch
 
 from . import _lib
-from .adaptive_attention import ATT, _Plan
+from .adaptive_attention import ATT
 
 
 class _Slot:
     def __init__(self, dev, stream):
         self.stream = stream
-        self._aux = None
         self.dev = dev
         self.ws = None
-        self.plans = collections.OrderedDict()  # images key -> _Plan
-        self.seen = set()
-
-    @property
-    def aux(self):
-        """The slot's side stream (aa_greedy_decode_aux's split LSTM steps), made on first use only:
-        an unused stream still takes a hardware queue in HIP's round-robin assignment."""
-        if self._aux is None:
-            from .hip_events import new_raw_stream
-            self._aux = new_raw_stream(self.dev)
-        return self._aux
 
 
 class Retired(tuple):
@@ -56,23 +44,22 @@ class DecodePipeline:
     """``for ids, alpha, beta in DecodePipeline(model, max_len=20).run(batches): ...`` — results
     in submission order, each exactly ``model.sampler(images, max_len)``'s.
 
-    ``graph=False`` (default) launches each batch's kernels directly into its slot's stream: the
-    process then owns exactly ``depth`` busy streams.  HIP multiplexes a process's streams onto a
-    few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and two slots that land on one queue
-    serialise; captured plans (``graph=True``) add the graph executor's own branch streams to that
-    count, which made the overlap hit-or-miss in measurements.
+    Each batch's kernels are launched directly into its slot's stream (one stream per slot: the
+    encoder's side branch stays on the slot stream, since the other slots already fill the chip), so
+    the process owns exactly ``depth`` busy streams.  HIP multiplexes a process's streams onto a few
+    hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and two slots that land on one queue
+    serialise.  (Slots replaying captured decode plans measured slower, DESIGN.md §4, and were
+    removed.)
 
     With ``raw_streams=True`` (default) the slots use the first ``depth`` of the process-wide list of
     fresh HIP streams (``hip_events.raw_streams``): two pipelines alive on one device share those
     streams and therefore serialise against each other (results stay correct; only their overlap is
     lost)."""
 
-    MAX_PLANS = 2
-
-    def __init__(self, model, max_len: int = 20, depth: int = 2, graph: bool = False, raw_streams: bool = True):
+    def __init__(self, model, max_len: int = 20, depth: int = 2, raw_streams: bool = True):
         if depth < 1:
             raise ValueError("depth must be >= 1")
-        self.model, self.T, self.depth, self.graph = model, int(max_len), int(depth), bool(graph)
+        self.model, self.T, self.depth = model, int(max_len), int(depth)
         self.raw_streams = bool(raw_streams)
         self._slots = None
         self._pending = collections.deque()
@@ -105,39 +92,21 @@ class DecodePipeline:
         ready.record()  # images (and any repack) are ready on the caller's stream
         s = slot.stream
         s.wait_event(ready)
-        if m.split_lstm:
-            slot.aux.wait_event(ready)
         images.record_stream(s)
         flags = m._decode_flags()  # the same flags sampler() passes (fp32_encoder included)
-        if self.graph and not m.split_lstm:  # a plan's side-stream branch would take one more queue
-            flags |= _lib.DECODE_ONE_STREAM
         with torch.cuda.device(dev), torch.cuda.stream(s):
-            key = (images.data_ptr(), B, T, m._packed.data_ptr(), flags)
-            plan = slot.plans.get(key) if self.graph else None
-            if plan is None and self.graph and key in slot.seen and B > 0 and T > 0:
-                s.synchronize()
-                plan = slot.plans[key] = _Plan(lib, model, images, B, T, flags, 1, m._c_dims(), dev)
-                while len(slot.plans) > self.MAX_PLANS:
-                    slot.plans.popitem(last=False)
-            slot.seen.add(key)
-            if plan is not None:
-                _lib.check(lib.aa_decode_plan_launch(plan.handle, s.cuda_stream), "decode_plan_launch")
-                out = (plan.ids.clone(), plan.alpha.clone(), plan.beta.clone())
-            else:
-                ids = torch.empty(B, T, dtype=torch.int64, device=dev)
-                alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
-                beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
-                nbytes = lib.aa_decode_workspace_bytes(m._c_dims(), B, T)
-                if nbytes and (slot.ws is None or slot.ws.numel() < nbytes):
-                    slot.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
-                                              beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None,
-                                              flags, s.cuda_stream,
-                                              # the other slots already fill the chip: one stream per slot
-                                              # unless the LSTM steps are split
-                                              slot.aux.cuda_stream if m.split_lstm else None)
-                _lib.check(rc, "greedy_decode")
-                out = (ids, alpha, beta)
+            ids = torch.empty(B, T, dtype=torch.int64, device=dev)
+            alpha = torch.empty(B, T, ATT, dtype=torch.float32, device=dev)
+            beta = torch.empty(B, T, 1, dtype=torch.float32, device=dev)
+            nbytes = lib.aa_decode_workspace_bytes(m._c_dims(), B, T)
+            if nbytes and (slot.ws is None or slot.ws.numel() < nbytes):
+                slot.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            # the other slots already fill the chip: one stream per slot (no aux stream)
+            rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
+                                          beta.data_ptr(), _lib.ptr(slot.ws) if nbytes else None, nbytes, None,
+                                          flags, s.cuda_stream, None)
+            _lib.check(rc, "greedy_decode")
+            out = (ids, alpha, beta)
             if ids_host is not None:
                 ids_host.copy_(out[0], non_blocking=True)
             done = torch.cuda.Event()

@@ -15,17 +15,25 @@ plus, for N > 1, the RCCL all-gather of the token ids (the path's only collectiv
 adaptive_amd.distributed.gather_rows), plus the ids device -> host copy.  Each rank
 decodes its own rows (weak scaling: global batch = 512 N).  Inputs are resident in HBM before the
 timed region.  ``value`` is SURVEY.md §8d's metric: captions / median wall time of one sampler()
-call after another (the reference's eval loop, code_src/tools/utils.py:167-171).  The same K
-batches with several in flight (adaptive_amd.pipeline.DecodePipeline, one distinct feature batch
-per batch in flight) are reported in ``pipelined``.  Every mode is timed over >= 5 regions of
-exactly K steps and the median region is reported.  Rank 0 prints ONE JSON line.
+call after another (direct kernel launches, as every caller gets them).  ``eval_loop``: the
+reference's own eval loop (code_src/tools/utils.py:23-29,167-171) -- a freshly allocated feature
+batch per call, filled by a device copy (the stand-in for ``to_var(images)``'s ``.cuda()``), then
+``model.sampler(images)`` and the ids to the host -- timed with events around the sampler call
+(``value``) and by wall clock including the fill.  The same K batches with several in flight
+(adaptive_amd.pipeline.DecodePipeline, one distinct feature batch per batch in flight) are reported
+in ``pipelined``.  Every mode is timed over >= 5 regions of exactly K steps and the median region is
+reported.  Rank 0 prints ONE JSON line.
 
 Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic bytes or FLOPs / its
-average HIP-event duration inside a traced region), ``kernels`` (all per-kernel averages),
-``hbm_frac_path`` (§8d: bytes(B) per step / step time / 8 TB/s), ``fp32_binding`` (§8d's binding
-figure F x captions/s / 157.3 TF), ``path_roofline`` (every kernel's work at its own ceiling,
-summed, over the measured time per batch), ``cpu_baseline`` (the PyTorch-CPU restatement of the
-reference sampler, oracle/adaptive_oracle.py, timed on this host's cores, rank 0, N=1).
+average duration by timing-only HIP events on its launch stream inside a traced region; for
+``k_atten`` the per-step re-read of V, which SURVEY.md §8d excludes from the algorithmic bytes, is
+priced separately against a MALL read ceiling measured here), ``kernels`` (all per-kernel averages),
+``path_traffic`` (PMC bytes of every launch of one decode, profiles/traffic.json, over §8d's
+algorithmic bytes), ``hbm_frac_path`` (§8d: bytes(B) per step / step time / 8 TB/s),
+``fp32_binding`` (§8d's binding figure F x captions/s / 157.3 TF), ``path_roofline`` (every
+kernel's work at its own ceiling, summed, over the measured time per batch), ``cpu_baseline`` (the
+PyTorch-CPU restatement of the reference sampler, oracle/adaptive_oracle.py, timed on this host's
+cores, rank 0, N=1).
 """
 from __future__ import annotations
 
@@ -52,7 +60,7 @@ from adaptive_amd.pipeline import DecodePipeline  # noqa: E402
 METRIC = "captions/sec (greedy, max_len=20) at B=512; 1/2/4/8-GPU scaling"
 PEAK_FP32 = 157.3e12     # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_BF16 = 2.5e15       # MI355X dense bf16 MFMA (no sparsity)
-PEAK_X3 = PEAK_BF16 / 6  # fp32 GEMM as six bf16 MFMA products of 3-way split operands (k_enc_v3)
+PEAK_X3 = PEAK_BF16 / 6  # fp32 GEMM as six bf16 MFMA products of 3-way split operands (bf16x3)
 PEAK_HBM = 8.0e12        # HBM3E spec
 E, H, V, C, P = 256, 512, 10123, 2048, 49
 
@@ -73,47 +81,36 @@ def flops_per_caption(T: int) -> dict:
             # pack-time token table and the once-per-batch x_g GEMM; k_lstm runs h W_hh^T and the
             # attention projections of h and s in its epilogue
             "xg": 2 * E * 5 * H, "k_lstm": 2 * H * 4 * H + proj, "k_vscreen": vocab,
-            # split LSTM step (aa_greedy_decode_aux): the GEMM alone, and the cell with the projections
             "k_lstm_gemm": 2 * H * 4 * H, "proj": proj}
 
 
 def kernel_costs(B: int, T: int) -> dict:
-    """Per-launch algorithmic cost of every kernel on the path: (bound, amount, unit-of-amount).
-    FLOPs for the MFMA kernels, bytes for the memory-bound ones."""
+    """Per-launch algorithmic cost of every kernel on the path: (bound, amount).  FLOPs for the MFMA
+    kernels, bytes for the memory-bound ones.  k_atten's amount is its HBM-algorithmic
+    bytes (V counted once per batch, at the encoder); its per-step re-read of V is
+    ``v_restream_bytes`` and priced separately."""
     f = flops_per_caption(T)
     return {
-        "k_avgpool": ("hbm", B * C * (P + 1) * 4),                       # read A once, write a_g
         "k_enc_v4": ("mfma_x3", f["k_enc_v"] * B),  # + the fused avg-pool (not priced)
-        "k_enc_v3": ("mfma_x3", f["k_enc_v"] * B),
-        "k_enc_heads": ("mfma", f["k_enc_heads"] * B),
         "k_gemm3(heads)": ("mfma_x3", f["k_enc_heads"] * B),
         "k_gemm3(VWv)": ("mfma_x3", f["vwv"] * B),
         "k_gemm3(x_g)": ("mfma_x3", f["xg"] * B),
-        "k_gemm_bias(VWv)": ("mfma", f["vwv"] * B),  # fp32-MFMA encoder builds (--enc-v3)
-        "k_gemm_bias(x_g)": ("mfma", f["xg"] * B),
         "k_lstm": ("mfma_x3", f["k_lstm"] * B),
-        "k_lstm_gemm": ("mfma_x3", f["k_lstm_gemm"] * B),
-        "k_lstm_cell": ("hbm", lstm_cell_bytes(B)),
-        "k_atten": ("hbm", atten_bytes_per_row() * B),
+        "k_atten": ("hbm", (atten_bytes_per_row() - v_restream_bytes_per_row()) * B),
         "k_vscreen": ("mfma_bf16", f["k_vscreen"] * B),
-        "k_vscreen3": ("mfma_bf16", f["k_vscreen"] * B),  # + the candidate lists (not priced)
         # per row: 320 granule summaries + u + the winning W_m row + id/key out (candidate count varies)
         "k_vrescore": ("hbm", B * ((V + 127) // 128 * 4 * 16 + 4 * H + 4 * H + 16)),
-        # per row: u + the winning W_m row + id/key out (the list and the other candidates vary)
-        "k_vrescore3": ("hbm", B * (4 * H + 4 * H + 16)),
     }
 
 
-def lstm_cell_bytes(B: int) -> int:
-    """k_lstm_cell algorithmic bytes per launch: per row the GEMM gates (4H), the token's table row
-    and the x_g row (5H each), c in; h, c, s out (+ h as 3 bf16 planes) and the H/16 tiles' 98
-    projection partials; per 64-row tile the W_g / W_s slices."""
-    per_row = 4 * (4 * H + 5 * H + 5 * H + H + 3 * H) + 2 * 3 * H + 4 * (H // 16) * 2 * P
-    return B * per_row + ((B + 63) // 64) * 4 * 2 * P * H
+def v_restream_bytes_per_row() -> int:
+    """k_atten's per-step re-read of the row's V (49 x H fp32): produced once by the encoder, so not
+    algorithmic bytes by SURVEY.md §8d; 51.4 MB per launch at B = 512, served from the MALL."""
+    return 4 * P * H
 
 
 def atten_bytes_per_row() -> int:
-    """k_atten algorithmic bytes per row: V rows + VWv rows + 32 projection partials of 98 + h, s in,
+    """k_atten bytes per row as executed: V rows + VWv rows + 32 projection partials of 98 + h, s in,
     u out (+ bf16 u), alpha/beta out."""
     return 4 * (P * H + P * P + (H // 16) * 2 * P + 2 * H + H + P + 1) + 2 * H
 
@@ -191,7 +188,7 @@ def path_bytes(B: int, T: int) -> int:
     return B * (C * (P + 1) * 4 + T * (8 + 4 * P + 4)) + 46_263_024 + min(B * T, V) * E * 4
 
 
-def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True, v_restream: bool = True) -> dict:
+def path_ideal_seconds(B: int, T: int, Vp: int = 10240, v_restream: bool = True) -> dict:
     """Work of one decode priced at each kernel's own ceiling: bf16x3 GEMMs at bf16
     peak / 6, fp32 MFMA GEMMs at the fp32 peak, the bf16 vocab screen (all Vp padded columns) at the
     bf16 peak, the attention and rescoring at HBM peak for their bytes.  The sum is the time a decode
@@ -209,9 +206,53 @@ def path_ideal_seconds(B: int, T: int, Vp: int = 10240, lists: bool = True, v_re
         "k_atten": T * atten_row * B / PEAK_HBM,
         "k_vscreen": T * 2 * H * Vp * B / PEAK_BF16,
     }
-    rescore = "k_vrescore3" if lists else "k_vrescore"
-    parts[rescore] = T * kernel_costs(B, T)[rescore][1] / PEAK_HBM
+    parts["k_vrescore"] = T * kernel_costs(B, T)["k_vrescore"][1] / PEAK_HBM
     return {"total": sum(parts.values()), "parts": parts}
+
+
+# rocprof names of the kernels one decode launches, with launches per decode (profiles/traffic.json)
+def path_launches(T: int) -> dict:
+    return {"k_enc_v4": 1, "k_gemm3": 3, "k_split_rows": 1, "k_decode_init": 1,
+            "k_lstm": T, "k_atten5": T, "k_vscreen2": T, "k_vrescore": T}
+
+
+def path_traffic(B: int, T: int, traffic_json: str) -> dict:
+    """PMC bytes of every launch of one decode (profiles/traffic.json, measured at B = 512 from
+    separate FETCH_SIZE / WRITE_SIZE passes) against SURVEY.md §8d's algorithmic bytes per batch."""
+    try:
+        with open(traffic_json) as f:
+            tr = json.load(f)
+    except Exception:
+        return None
+    per = {k: n * tr[k]["hbm_bytes_per_launch"] for k, n in path_launches(T).items() if k in tr}
+    missing = [k for k in path_launches(T) if k not in tr]
+    total = sum(per.values())
+    return {"pmc_bytes_per_batch": total, "algorithmic_bytes_per_batch": path_bytes(B, T),
+            "ratio": total / path_bytes(B, T), "by_kernel": per, "missing": missing,
+            "source": os.path.relpath(traffic_json, ROOT),
+            "note": "bytes that left L2 ((2 FETCH_SIZE + WRITE_SIZE) x 1 KiB per launch, MALL hits included) "
+                    "over inputs + outputs + every weight once; the excess is step-invariant operands "
+                    "re-streamed every step (V, W_hh fragments, W_m bf16)"}
+
+
+def read_probe(dev, nbytes: int, reps: int = 20) -> float:
+    """Streaming read rate (GB/s) of a resident ``nbytes`` buffer, re-read back to back (aa_read_probe,
+    timing-only events around ``reps`` launches after one warm pass): for a buffer that fits the
+    256 MiB Infinity Cache, the MALL-served read ceiling."""
+    lib = _lib.load()
+    buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    blocks = 2048
+    out = torch.empty(blocks, dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ev = EventArray(2)
+    for _ in range(3):
+        _lib.check(lib.aa_read_probe(buf.data_ptr(), nbytes, out.data_ptr(), blocks, s.cuda_stream), "read_probe")
+    ev.record(0, s)
+    for _ in range(reps):
+        _lib.check(lib.aa_read_probe(buf.data_ptr(), nbytes, out.data_ptr(), blocks, s.cuda_stream), "read_probe")
+    ev.record(1, s)
+    ms = ev.elapsed_ms(0, 1)
+    return nbytes * reps / (ms * 1e-3) / 1e9
 
 
 def spawn_ranks(n: int, argv: list) -> int:
@@ -288,29 +329,14 @@ def main():
     ap.add_argument("--max-len", type=int, default=20)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--lanes", type=int, default=None, help="HIP streams the step loop is split over "
-                    "(default: the model's decode_lanes)")
-    ap.add_argument("--no-graph", action="store_true", help="launch kernels directly instead of replaying the "
-                    "captured decode plan (hipGraph)")
     ap.add_argument("--no-trace", action="store_true", help="skip the per-kernel HIP events")
-    ap.add_argument("--pipeline-depth", type=int, default=3, help="batches in flight in the headline region "
+    ap.add_argument("--no-eval-loop", action="store_true", help="skip the fresh-allocation eval-loop leg")
+    ap.add_argument("--pipeline-depth", type=int, default=3, help="batches in flight in the `pipelined` region "
                     "(adaptive_amd.pipeline.DecodePipeline: batch i+1 starts on its own stream while batch i "
-                    "finishes); 1 = one sampler() call after another")
-    ap.add_argument("--split-lstm", action="store_true", help="split LSTM steps: k_lstm_gemm on a side stream "
-                    "+ k_lstm_cell instead of the one-launch k_lstm (same results; slower at B=512)")
-    ap.add_argument("--screen64", action="store_true", help="vocab screen on 64x64 tiles (k_vscreen) instead of "
-                    "128x160 (k_vscreen2)")
-    ap.add_argument("--vocab-lists", action="store_true", help="vocab stage as per-row candidate lists (k_vscreen3) "
-                    "+ k_vrescore3 instead of granule summaries (k_vscreen2) + k_vrescore (same ids)")
-    ap.add_argument("--enc-v3", action="store_true", help="encoder V GEMM on k_enc_v3 (128x128 tiles) instead of "
-                    "k_enc_v4 (two images per workgroup, all columns)")
+                    "finishes); 1 = no pipelined region")
     ap.add_argument("--no-d2h", action="store_true", help="diagnostics: leave the ids on the device (not the metric)")
     ap.add_argument("--single-buffer", action="store_true", help="diagnostics: every batch reads the same feature "
                     "buffer (MALL-resident; not the metric)")
-    ap.add_argument("--replicate-buffer", action="store_true", help="diagnostics: distinct feature buffers holding "
-                    "copies of the same batch (not the metric)")
-    ap.add_argument("--pipeline-graph", action="store_true", help="pipeline slots replay captured one-stream "
-                    "decode plans (hipGraph) instead of launching kernels directly")
     ap.add_argument("--pool-streams", action="store_true", help="pipeline slots on torch pool streams instead of "
                     "freshly created HIP streams")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
@@ -345,13 +371,9 @@ def main():
 
     B, T = args.batch, args.max_len
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
-    model.split_lstm = args.split_lstm
-    model.screen64 = args.screen64
-    model.vocab_lists = args.vocab_lists
-    lists = args.vocab_lists and not args.screen64
-    screen_name, rescore_name = ("k_vscreen3", "k_vrescore3") if lists else ("k_vscreen", "k_vrescore")
-    model.enc_v3 = args.enc_v3
-    enc_name = "k_enc_v3" if args.enc_v3 else "k_enc_v4"
+    # one process per GPU: this rank's sampler() stays on its own device (the single-process
+    # multi-device mode, on by default when several GPUs are visible, is not what a rank measures)
+    model.device_parallel = False
     depth = max(1, args.pipeline_depth)
     # distinct resident feature batches: each batch in flight reads its own 205 MB
     # map, so nothing is served from the 256 MB MALL left behind by the previous batch.  Buffer 0 is
@@ -359,11 +381,7 @@ def main():
     # seeds 1.. for the same rows.
     nbuf = 1 if args.single_buffer else max(depth, 2)
     bufs = [synthetic_features(B, dev, seed=i, row0=rank * B) for i in range(nbuf)]
-    model.MAX_PLANS = max(model.MAX_PLANS, nbuf)  # one captured decode plan per resident buffer
     feats = bufs[0]
-    if args.replicate_buffer:
-        for b_ in bufs[1:]:
-            b_.copy_(feats)
     host_ids = [torch.empty(world * B, T, dtype=torch.int64, pin_memory=True) for _ in range(2)]
     # one-GPU pipelined region: each batch's ids leave on its own slot stream (DecodePipeline(ids_host)),
     # so the caller's stream carries no copies between the slots' batches
@@ -378,12 +396,10 @@ def main():
             host_ids[i & 1].copy_(ids, non_blocking=True)
 
     def step(i, trace=None):
-        ids, alpha, beta = model.sampler(bufs[i % nbuf], max_len=T, trace=trace, lanes=args.lanes,
-                                         graph=not args.no_graph)
+        ids, alpha, beta = model.sampler(bufs[i % nbuf], max_len=T, trace=trace)
         finish(i, ids)
 
-    pipe = DecodePipeline(model, max_len=T, depth=depth, raw_streams=not args.pool_streams,
-                          graph=args.pipeline_graph)
+    pipe = DecodePipeline(model, max_len=T, depth=depth, raw_streams=not args.pool_streams)
 
     def pipelined(n):
         if world == 1 and not args.no_d2h:
@@ -394,40 +410,67 @@ def main():
             finish(i, ids)
 
     K = args.steps
-    # untimed warm-up: every buffer seen twice (its decode plan is captured), then one region's worth
-    # of sequential steps and four of pipelined batches (the first pipelined regions otherwise ran 5-10 %
-    # low, settling after ~150 batches)
-    for i in range(max(args.warmup, 3 * nbuf, K)):
+    eval_ev = EventArray(2 * K)
+    cur = torch.cuda.current_stream(dev)
+
+    def eval_loop(n):
+        """The reference's coco_eval loop (utils.py:167-171): every call gets a FRESHLY allocated batch
+        (torch's caching allocator hands back the block the previous batch freed, as it does there),
+        filled by a device copy standing in for to_var(images)'s .cuda(); sampler(); ids to the host.
+        Timing-only events bracket each sampler call + ids copy."""
+        for i in range(n):
+            x = torch.empty_like(feats)
+            x.copy_(bufs[i % nbuf])
+            eval_ev.record(2 * i, cur)
+            ids, _, _ = model.sampler(x, max_len=T)
+            finish(i, ids)
+            eval_ev.record(2 * i + 1, cur)
+            del x, ids
+
+    # untimed warm-up: K sequential steps, the eval loop, then four regions' worth of pipelined
+    # batches (the first pipelined regions otherwise ran 5-10 % low, settling after ~150 batches)
+    for i in range(max(args.warmup, 2 * nbuf, K)):
         step(i)
-    pipelined(max(args.warmup, 2 * depth + 1, 4 * K))
+    if not args.no_eval_loop:
+        eval_loop(K)
+    if depth > 1:
+        pipelined(max(args.warmup, 2 * depth + 1, 4 * K))
+    kern = ("lstm", "atten", "screen", "rescore")
     traces = []
     if not args.no_trace:
         for _ in range(K):
-            ev = {k: EventArray(2 * T) for k in ("lstm", "atten", "screen", "rescore", "gemm")}
+            ev = {k: EventArray(2 * T) for k in kern}
             ev["encoder"] = EventArray(2 * _lib.TRACE_ENCODER_KERNELS)
             tr = _lib.Trace(ev["encoder"].ptr, ev["lstm"].ptr, ev["atten"].ptr, ev["screen"].ptr, ev["rescore"].ptr,
-                            ev["gemm"].ptr if model.split_lstm else None)
+                            None)
             traces.append((ev, tr))
 
-    def timed(trace_list, pipeline=False):
+    def timed(trace_list=None, mode="sequential"):
         def run():
-            if pipeline:
+            if mode == "pipelined":
                 pipelined(K)
+            elif mode == "eval_loop":
+                eval_loop(K)
             else:
                 for k in range(K):
                     step(k, trace_list[k][1] if trace_list else None)
         return time_region(run, world, torch.cuda.synchronize, dev)
 
     # Regions: `--regions` (>= 5) timed regions of exactly K steps each for the sequential sampler
-    # calls (the headline) and, when depth > 1, for DecodePipeline (``pipelined``);
-    # each mode reports its median region.  Then one more region of the K sequential steps with a HIP
-    # event pair around every kernel launch (on its launch stream) for the per-kernel averages;
-    # events are timestamp packets in the queue, so that region runs a little slower and is reported
-    # separately as ``traced_ms_per_step``.
+    # calls (the headline, SURVEY.md §8d), the eval loop and, when depth > 1, DecodePipeline; each mode
+    # reports its median region.  Then one more region of the K sequential steps with a timing-only
+    # event pair around every kernel launch (on its launch stream) for the per-kernel averages,
+    # reported separately as ``traced_ms_per_step``.
     R = max(5, args.regions)
-    seq_regions = [timed(None) for _ in range(R)]
+    seq_regions = [timed() for _ in range(R)]
     log(f"sequential regions (s): {seq_regions}")
-    pipe_regions = [timed(None, pipeline=True) for _ in range(R)] if depth > 1 else seq_regions
+    eval_regions, eval_sampler_s = [], []
+    if not args.no_eval_loop:
+        for _ in range(R):
+            eval_regions.append(timed(mode="eval_loop"))
+            eval_sampler_s.append(sum(eval_ev.pair_durations_ms()) * 1e-3)
+        log(f"eval-loop regions (s): wall {eval_regions}, sampler events {eval_sampler_s}")
+    pipe_regions = [timed(mode="pipelined") for _ in range(R)] if depth > 1 else seq_regions
     log(f"pipelined regions (s): {pipe_regions}")
     elapsed = float(np.median(seq_regions))
     elapsed_pipe = float(np.median(pipe_regions))
@@ -439,25 +482,15 @@ def main():
     kernels = {}
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
-        lstm = "k_lstm_cell" if model.split_lstm else "k_lstm"
-        enc_names = (("k_avgpool", enc_name, "k_enc_heads", "k_gemm_bias(VWv)", "k_gemm_bias(x_g)") if args.enc_v3
-                     else ("k_avgpool", enc_name, "k_gemm3(heads)", "k_gemm3(VWv)", "k_gemm3(x_g)"))
-        per = {k: [] for k in enc_names + (lstm, "k_atten", screen_name, rescore_name)}
-        if not args.enc_v3:
-            del per["k_avgpool"]  # fused into k_enc_v4 (its trace pair is empty)
-        if model.split_lstm:
-            per["k_lstm_gemm"] = []
+        enc_names = ("k_avgpool", "k_enc_v4", "k_gemm3(heads)", "k_gemm3(VWv)", "k_gemm3(x_g)")
+        per = {k: [] for k in enc_names[1:] + ("k_lstm", "k_atten", "k_vscreen", "k_vrescore")}
         for ev, _ in traces:
             enc = ev["encoder"].pair_durations_ms()
             for i, k in enumerate(enc_names):
-                if k in per:
+                if k in per:  # (k_avgpool is fused into k_enc_v4: its trace pair is empty)
                     per[k].append(enc[i])
-            per[lstm] += ev["lstm"].pair_durations_ms()
-            if model.split_lstm:
-                per["k_lstm_gemm"] += ev["gemm"].pair_durations_ms()
-            per["k_atten"] += ev["atten"].pair_durations_ms()
-            per[screen_name] += ev["screen"].pair_durations_ms()
-            per[rescore_name] += ev["rescore"].pair_durations_ms()
+            for k, name in zip(kern, ("k_lstm", "k_atten", "k_vscreen", "k_vrescore")):
+                per[name] += ev[k].pair_durations_ms()
         costs = kernel_costs(B, T)
         for k, ds in per.items():
             avg_ms = float(np.mean(ds))
@@ -478,29 +511,58 @@ def main():
                                      "(fp32-accurate); algorithmic fp32 FLOPs priced against bf16 peak / 6")
                 if bound == "mfma_bf16":
                     entry["note"] = ("2HV vocab contraction on bf16 MFMA under a rigorous error bound (exact fp32 "
-                                     "rescoring of the candidates in " + rescore_name + "); priced against the "
-                                     "dense bf16 peak")
+                                     "rescoring of the candidates in k_vrescore); priced against the dense bf16 peak")
             entry["frac"] = entry["achieved"] / entry["peak"]
             kernels[k] = entry
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
     roofline = None
+    traffic_all = {}
+    try:
+        with open(args.traffic_json) as f:
+            traffic_all = json.load(f)
+    except Exception:
+        pass
     if dominant:
         kd = kernels[dominant]
-        traffic = None
-        pmc_name = {"k_atten": "k_atten5", "k_vscreen": "k_vscreen2"}.get(dominant, dominant)  # rocprof names
-        try:
-            with open(args.traffic_json) as f:
-                traffic = json.load(f).get(pmc_name, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            pass
+        pmc_name = {"k_atten": "k_atten5", "k_vscreen": "k_vscreen2"}.get(dominant, dominant.split("(")[0])
+        traffic = traffic_all.get(pmc_name, {}).get("hbm_bytes_per_launch")
         roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
-                    "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"]}
+                    "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"],
+                    "duration_source": "timing-only HIP events (hipEventDisableSystemFence | hipEventReleaseToDevice) "
+                                       "on the launch stream around each launch, traced region"}
+        if dominant == "k_atten":
+            vb = v_restream_bytes_per_row() * B
+            mall = read_probe(dev, vb)
+            sec = kd["avg_ms"] * 1e-3
+            roofline["algorithmic_bytes_per_launch"] = kd["algorithmic_bytes_per_launch"]
+            roofline["v_restream"] = {
+                "bytes_per_launch": vb, "achieved_gbs": vb / sec / 1e9,
+                "mall_read_ceiling_gbs": mall, "frac_of_mall_ceiling": vb / sec / 1e9 / mall,
+                "executed_bytes_per_launch": kd["algorithmic_bytes_per_launch"] + vb,
+                "executed_achieved_gbs": (kd["algorithmic_bytes_per_launch"] + vb) / sec / 1e9,
+                "note": "the per-step re-read of V (not algorithmic bytes, SURVEY.md §8d; 51.4 MB at B=512, "
+                        "MALL-resident), priced against the MALL-served read rate of a V-sized buffer "
+                        "measured here (aa_read_probe, re-read back to back)"}
 
-    ideal = path_ideal_seconds(B, T, lists=lists, v_restream=False)
-    ideal_exec = path_ideal_seconds(B, T, lists=lists, v_restream=True)
+    ideal = path_ideal_seconds(B, T, v_restream=False)
+    ideal_exec = path_ideal_seconds(B, T, v_restream=True)
     F = flops_per_caption(T)["total"]
     per_gpu_rate, per_gpu_rate_pipe = value / world, captions / elapsed_pipe / world
+    eval_block = None
+    if eval_regions:
+        ev_wall = float(np.median(eval_regions))
+        ev_sampler = float(np.median(eval_sampler_s))
+        eval_block = {"value": captions / ev_sampler, "value_incl_fill": captions / ev_wall,
+                      "frac_of_value": captions / ev_sampler / value,
+                      "ms_per_step": 1e3 * ev_sampler / K, "ms_per_step_incl_fill": 1e3 * ev_wall / K,
+                      "regions_captions_per_s": [captions / e for e in eval_sampler_s],
+                      "captures": Encoder2Decoder._captures,
+                      "note": "code_src/tools/utils.py:167-171 as called: a freshly allocated [B,2048,7,7] batch per "
+                              "sampler() call (filled by a device copy standing in for to_var(images).cuda(), whose "
+                              "PCIe transfer is outside the metric, DESIGN.md §7), ids to the host; `value` times the "
+                              "sampler call + ids copy by timing-only events, `value_incl_fill` the whole loop by "
+                              "wall clock"}
     out = {
         "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -511,23 +573,18 @@ def main():
                    "batch_per_gpu": B, "global_batch": world * B, "max_len": T, "hidden": H, "embed": E,
                    "vocab": V, "parallelism": f"dp{world}" + ("+allgather(ids)" if world > 1 else "")
                    + ("" if backend == "nccl" else f" ({backend} rehearsal)"),
-                   "lanes": args.lanes if args.lanes is not None else model.decode_lanes,
                    "batches_in_flight": 1, "feature_buffers": nbuf,
-                   # how each region launches: the headline's sampler() calls replay captured decode
-                   # plans; the pipeline's slots launch kernels directly (its graph=False default)
-                   "hip_graph": {"sequential": not args.no_graph, "pipelined": pipe.graph},
-                   "vocab_stage": "k_vscreen3 (screen + per-row candidate lists) + k_vrescore3" if lists
-                   else "k_vscreen2/k_vscreen (granule summaries) + k_vrescore",
-                   "lstm_step": "split (k_lstm_gemm on a side stream + k_lstm_cell)" if model.split_lstm
-                   else "fused (k_lstm)",
+                   "launch": "direct kernel launches from one C call per sampler() (no hipGraph, no per-buffer cache)",
+                   "vocab_stage": "k_vscreen2 (bf16 screen, granule summaries) + k_vrescore (exact fp32 rescoring)",
                    "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy",
-                   "headline": "one sampler() call after another (the reference's eval loop, utils.py:167-171)"},
+                   "headline": "one sampler() call after another on resident batches"},
         "ranks_seen": dist.get_world_size() if world > 1 else 1,
         "backend": (dist.get_backend() if world > 1 else None),
         "regions": {"count": R, "sequential_captions_per_s": [captions / e for e in seq_regions],
                     "pipelined_captions_per_s": [captions / e for e in pipe_regions], "reported": "median"},
+        "eval_loop": eval_block,
         "pipelined": {"value": captions / elapsed_pipe, "ms_per_step": 1e3 * elapsed_pipe / K,
-                      "batches_in_flight": depth, "hip_graph": pipe.graph,
+                      "batches_in_flight": depth,
                       "note": "the same K batches with `batches_in_flight` in flight through "
                               "adaptive_amd.pipeline.DecodePipeline (each batch its own resident features, "
                               "its ids copied to the host on its own stream); an API the reference does not call"},
@@ -536,6 +593,7 @@ def main():
         "hbm_frac_path": path_bytes(B, T) * per_gpu_rate / B / PEAK_HBM,
         "hbm_frac_path_pipelined": path_bytes(B, T) * per_gpu_rate_pipe / B / PEAK_HBM,
         "path_bytes_per_batch": path_bytes(B, T),
+        "path_traffic": path_traffic(B, T, args.traffic_json),
         # SURVEY.md §8d's binding figure: F = 415,361,744 FLOP per caption against the fp32 peak
         "fp32_binding": {"flops_per_caption": F, "achieved_tflops": F * per_gpu_rate / 1e12,
                          "peak_tflops": PEAK_FP32 / 1e12, "frac": F * per_gpu_rate / PEAK_FP32,

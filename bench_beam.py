@@ -61,15 +61,12 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--tile128", action="store_true", help="vocab logits on 128x128 tiles (k_vbeam4) instead of "
-                    "256x256 (k_vbeam5)")
     ap.add_argument("--fast", action="store_true", help="opt-in bf16x3 logits (AA_BEAM_FAST) instead of the exact "
                     "fp32 default")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, K, T = args.batch, args.beam, args.T
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
-    model.beam_tile128 = args.tile128
     feats = synthetic_features(B, dev, seed=0)
     for _ in range(args.warmup):
         model.beam_search(feats, T, K, fast=args.fast)
@@ -91,7 +88,7 @@ def main():
     Vn, H = model.dims.vocab, model.dims.hidden
     flops = 2.0 * B * K * Vn * H  # algorithmic: the [B K, H] x [H, V] logits GEMM of one step
     peak = PEAK_X3 if args.fast else PEAK_FP32
-    kname = ("k_vbeam4" if args.tile128 else "k_vbeam5") if args.fast else "k_vexact"
+    kname = "k_vbeam5" if args.fast else "k_vexact"
     traffic = None
     try:
         with open(os.path.join(ROOT, "profiles", "traffic_beam.json")) as f:
@@ -110,7 +107,7 @@ def main():
            "data": "synthetic: U[0,1) post-trunk features, random-init weights (adaptive_amd.synth seed 123)",
            "config": {"workload": f"Encoder2Decoder.beam_search B={B} beam={K} max_len={T}", "batch": B,
                       "beam": K, "T": T, "rows": B * K,
-                      "vocab_kernel": ("bf16x3 " + ("k_vbeam4 (128x128)" if args.tile128 else "k_vbeam5 (256x256)"))
+                      "vocab_kernel": "bf16x3 k_vbeam5 (256x256)"
                       if args.fast else "exact fp32: k_vexact (fused fp32 MFMA logits + granule summaries)",
                       "mode": "fast (opt-in bf16x3)" if args.fast else "exact (default)"},
            "best_score_mean": float(out[4][:, 0].mean().item()), "roofline": roofline, "cpu_baseline": None}

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 14
+#define AA_ABI_VERSION 15
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -121,12 +121,9 @@ typedef struct aa_model {
  *   encoder_events: 2*AA_TRACE_ENCODER_KERNELS events, launches in the order
  *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
  *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen2 /
- *                   k_vscreen (k_vscreen3 under AA_DECODE_LISTS, k_vocab under
- *                   AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (k_vrescore3; unused under
- *                   AA_DECODE_EXACT_VOCAB);
- *                   lstm = k_lstm, or k_lstm_cell when the step is split (aa_greedy_decode_aux);
- *   gemm_events:    2*T events, launch i = k_lstm_gemm of step i (split steps only; recorded on
- *                   the aux stream). */
+ *                   k_vscreen (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused
+ *                   under AA_DECODE_EXACT_VOCAB); lstm = k_lstm;
+ *   gemm_events:    unused (kept for layout stability; may be NULL). */
 #define AA_TRACE_ENCODER_KERNELS 5
 typedef struct aa_trace {
   aa_event_t* encoder_events;
@@ -179,21 +176,10 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 /* Decode flags */
 #define AA_DECODE_EXACT_VOCAB 1 /* compute every fp32 logit (fp32 MFMA GEMM + fused argmax) instead of
                                    the bf16 screen + exact fp32 rescoring; both give the same ids */
-#define AA_DECODE_SCREEN64 8 /* vocab screen on 64 x 64 tiles (k_vscreen) instead of the 128 x 160 tiles of
-                                k_vscreen2 (same summaries up to fp32 summation order; same ids) */
-#define AA_DECODE_FUSED_LSTM 4 /* aa_greedy_decode_aux / decode plans: keep the one-launch LSTM step
-                                  (k_lstm) instead of the split k_lstm_gemm + k_lstm_cell */
 #define AA_DECODE_FP32_ENCODER 2 /* V = relu(A W_a^T + b) on fp32 MFMA (v_mfma_f32_32x32x2f32) instead of
                                     the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v4) */
-#define AA_BEAM_TILE128 64 /* beam search: vocab logits on 128 x 128 tiles (k_vbeam4) instead of 256 x 256
-                             (k_vbeam5); identical logits */
-#define AA_DECODE_LISTS 32 /* greedy: the vocab screen appends per-row candidate lists against a running max
-                             lower bound (k_vscreen3) and k_vrescore3 rescores them, instead of granule
-                             summaries (k_vscreen2) + k_vrescore; same ids (measured slower at B = 512) */
 #define AA_DECODE_ONE_STREAM 512 /* decode plans: capture the whole decode on one stream (no side-stream
                                      branch for the encoder's a_g work); for several plans in flight */
-#define AA_DECODE_ENC_V3 16 /* V on the 128 x 128-tile bf16x3 kernel (k_enc_v3) instead of k_enc_v4 (one
-                               workgroup per two images, all H columns; H in {256, 512}) */
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];
@@ -208,43 +194,27 @@ AA_API int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, in
                             size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                             aa_stream_t stream);
 
-/* aa_greedy_decode with a second stream `aux_stream` for work off the step chain: the encoder's
- * a_g branch (avgpool, heads, x_g GEMM) beside the V branch, and every LSTM step split in two --
- * k_lstm_gemm (h_{t-1} W_hh^T, which needs no token) for step t+1 runs on aux_stream beside step
- * t's attention, vocab screen and rescoring on `stream`, then k_lstm_cell of step t+1 (token
- * gather, cell, sentinel, projections) waits for it.  Same arithmetic in the same order as the
- * one-launch k_lstm, so the results equal aa_greedy_decode's bit for bit.  Fork/join through
- * events: the call is complete (and graph-capturable) on `stream`.  aux_stream NULL or equal to
- * `stream`: aa_greedy_decode.  flags & AA_DECODE_FUSED_LSTM keeps k_lstm. */
+/* aa_greedy_decode with a second stream `aux_stream` for the encoder's a_g branch (heads, x_g GEMM)
+ * beside the V branch's VWv GEMM.  Fork/join through events: the call is complete (and
+ * graph-capturable) on `stream`.  aux_stream NULL or equal to `stream`: aa_greedy_decode.  The
+ * results equal aa_greedy_decode's bit for bit. */
 AA_API int aa_greedy_decode_aux(const aa_model* m, const float* feats, int32_t B, int32_t T,
                                 int64_t* ids, float* alpha, float* beta, void* workspace,
                                 size_t workspace_bytes, const aa_trace* trace, int32_t flags,
                                 aa_stream_t stream, aa_stream_t aux_stream);
 
-/* aa_greedy_decode with the T-step loop split over up to AA_MAX_LANES streams ("lanes"): the
- * encoder tail runs on `stream` for the whole batch, then lane i decodes its contiguous block of
- * rows (whole 64-row tiles) on lanes[i], and `stream` waits for every lane before returning
- * (fork/join through events, so the call is graph-capturable from `stream`).  Captions are
- * independent, so the results equal aa_greedy_decode's bit for bit; the lanes' kernels overlap
- * on the GPU.  trace (if any) times lane 0.  n_lanes = 0 is aa_greedy_decode. */
-#define AA_MAX_LANES 8
-AA_API int aa_greedy_decode_lanes(const aa_model* m, const float* feats, int32_t B, int32_t T,
-                                  int64_t* ids, float* alpha, float* beta, void* workspace,
-                                  size_t workspace_bytes, const aa_trace* trace, int32_t flags,
-                                  aa_stream_t stream, const aa_stream_t* lanes, int32_t n_lanes);
-
-/* Decode plan: the complete greedy decode for fixed (B, T, flags, lanes) and fixed buffers,
- * captured once into a hipGraph (one graph launch replaces the ~4T+6 kernel launches; lanes, if
- * n_lanes > 1, are streams owned by the plan).  Launch it as often as needed on any stream; the
- * buffers it was created with are read/written at every launch.  Results equal aa_greedy_decode's
- * bit for bit.  With n_lanes <= 1 the plan captures aa_greedy_decode_aux's two-stream form (split
- * LSTM steps) unless flags & AA_DECODE_FUSED_LSTM.  The plan holds no device memory of its own
- * besides the instantiated graph. */
+/* Decode plan: the complete greedy decode for fixed (B, T, flags) and fixed buffers, captured once
+ * into a hipGraph (one graph launch replaces the ~4T+6 kernel launches).  Launch it as often as
+ * needed on any stream; the buffers it was created with -- feats included -- are read/written at
+ * every launch, so the caller owns them for the plan's lifetime (adaptive_amd.DecodePlan owns its
+ * own input buffer and copies each batch into it).  Results equal aa_greedy_decode's bit for bit.
+ * The plan captures aa_greedy_decode_aux's two-stream encoder unless flags &
+ * AA_DECODE_ONE_STREAM.  It holds no device memory of its own besides the instantiated graph;
+ * destroy it only after its last launch has completed. */
 typedef struct aa_decode_plan aa_decode_plan;
 AA_API int aa_decode_plan_create(const aa_model* m, const float* feats, int32_t B, int32_t T,
                                  int64_t* ids, float* alpha, float* beta, void* workspace,
-                                 size_t workspace_bytes, int32_t flags, int32_t n_lanes,
-                                 aa_decode_plan** plan);
+                                 size_t workspace_bytes, int32_t flags, aa_decode_plan** plan);
 AA_API int aa_decode_plan_launch(const aa_decode_plan* plan, aa_stream_t stream);
 AA_API int aa_decode_plan_destroy(aa_decode_plan* plan);
 
@@ -344,7 +314,8 @@ AA_API int aa_vocab_logits_at(const aa_model* m, int32_t B, const float* u, cons
  * ignore_index makes the loss NaN (torch raises a device-side assert).  Deterministic (fixed-order
  * reductions).  aa_cross_entropy_backward: dlogits = (softmax(x_i) - onehot(t_i)) * dloss[0] /
  * count[0] (0 for ignored rows), dloss a DEVICE scalar (the incoming gradient of the loss), with the
- * forward's workspace; dlogits may alias logits only if lddx == ldx. */
+ * forward's workspace (workspace_bytes >= aa_cross_entropy_workspace_bytes(N), else AA_ERR_BUFFER);
+ * dlogits may alias logits (in place) only if lddx == ldx (else AA_ERR_SHAPE). */
 AA_API size_t aa_cross_entropy_workspace_bytes(int32_t N);
 AA_API int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, int64_t ldx,
                                     const int64_t* targets, int64_t ignore_index, float* loss,
@@ -352,8 +323,8 @@ AA_API int aa_cross_entropy_forward(const float* logits, int32_t N, int32_t V, i
                                     aa_stream_t stream);
 AA_API int aa_cross_entropy_backward(const float* logits, int32_t N, int32_t V, int64_t ldx,
                                      const int64_t* targets, int64_t ignore_index, const float* dloss,
-                                     const float* count, const void* workspace, float* dlogits,
-                                     int64_t lddx, aa_stream_t stream);
+                                     const float* count, const void* workspace, size_t workspace_bytes,
+                                     float* dlogits, int64_t lddx, aa_stream_t stream);
 
 /* aa_adam_step: one torch.optim.Adam step (model_factory.py:71: Adam(params, lr, betas, weight_decay); amsgrad=False,
  * maximize=False, L2 weight_decay added to the gradient) over n fp32 tensors, every tensor in one
@@ -371,6 +342,12 @@ typedef struct aa_adam_tensor {
 } aa_adam_tensor;
 AA_API int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double lr, double beta1,
                         double beta2, double eps, double weight_decay, aa_stream_t stream);
+
+/* Measurement helper (bench.py's roofline block; not on the decode path): one streaming read of
+ * nbytes (multiple of 16, 16-B aligned) from src by `blocks` workgroups, each writing its partial sum
+ * to out[block].  Timed over a buffer resident in the 256 MiB Infinity Cache it gives the MALL-served
+ * read ceiling that the attention's per-step re-read of V is priced against. */
+AA_API int aa_read_probe(const void* src, size_t nbytes, float* out, int32_t blocks, aa_stream_t stream);
 
 /* Counter-based synthetic data (same bits as adaptive_amd/synth.py):
  * dst[i] = fp32(lo + (hi - lo) * u(key, start + i)), u = (splitmix64(key + (start+i+1)*GOLDEN) >> 40) / 2^24.

@@ -1,5 +1,6 @@
 """CPU: the C-ABI library loads and exports exactly what include/adaptive_amd.h declares, and the
 host-side queries (no device work) behave.  No compute calls: there is no GPU here."""
+import ctypes
 import os
 import re
 import subprocess
@@ -69,10 +70,16 @@ def test_argument_errors_without_device_work(lib):
     assert lib.aa_greedy_decode(m, None, 0, 20, None, None, None, None, 0, None, 0, None) == 0   # empty batch
     assert lib.aa_greedy_decode(m, None, 4, 20, None, None, None, None, 0, None, 0, None) == -1
     assert b"too small" in lib.aa_error_string(-4)
-    # lane-split variant: same argument checks, plus lanes
-    assert lib.aa_greedy_decode_lanes(m, None, 4, 20, None, None, None, None, 0, None, 0, None, None, -1) == -3
-    assert lib.aa_greedy_decode_lanes(m, None, 0, 20, None, None, None, None, 0, None, 0, None, None, 2) == 0
-    assert lib.aa_greedy_decode_lanes(m, 256, 4, 20, 256, None, None, 256, 10 ** 9, None, 0, None, None, 2) == -1
+    # the two-stream form: same argument checks
+    assert lib.aa_greedy_decode_aux(m, None, -1, 1, None, None, None, None, 0, None, 0, None, None) == -3
+    assert lib.aa_greedy_decode_aux(m, None, 0, 20, None, None, None, None, 0, None, 0, None, None) == 0
+    assert lib.aa_greedy_decode_aux(m, 256, 4, 20, None, None, None, 256, 10 ** 9, None, 0, None, None) == -1
+    # decode plans: shape and pointer checks before any capture
+    h = ctypes.c_void_p()
+    assert lib.aa_decode_plan_create(m, 256, 0, 20, 256, None, None, 256, 10 ** 9, 0, ctypes.byref(h)) == -3
+    assert lib.aa_decode_plan_create(m, None, 4, 20, 256, None, None, 256, 10 ** 9, 0, ctypes.byref(h)) == -1
+    assert lib.aa_decode_plan_create(m, 256, 4, 20, 256, None, None, 256, 10 ** 9, 0, None) == -1
+    assert h.value is None
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):

@@ -133,19 +133,20 @@ def test_beam_config4_b512_equals_oracle_on_64_images(gpu_device):
     np.testing.assert_allclose(be[:64].cpu().numpy(), o_be.numpy(), atol=ATT_TOL, rtol=0)
 
 
-def test_beam_tile256_equals_tile128(gpu_device):
-    """Fast mode: k_vbeam5 (256 x 256 tiles, used when the padded vocabulary is whole 256-column
-    tiles) and k_vbeam4 (128 x 128) run the same per-element product order: bit-identical beams."""
-    m = _model(gpu_device, _weights(end_boost=2.6))
-    f = torch.from_numpy(synth.make_features(200, seed=8)).to(gpu_device)
-    a = m.beam_search(f, 12, 3, fast=True)
-    m.beam_tile128 = True
-    try:
-        b = m.beam_search(f, 12, 3, fast=True)
-    finally:
-        m.beam_tile128 = False
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
+def test_beam_fast_tile128_vocab_vs_oracle(gpu_device):
+    """Fast mode on a vocabulary that is not whole 256-column tiles (3001 -> 3072 padded): the
+    128 x 128-tile k_vbeam4 runs instead of k_vbeam5; the beams agree with the oracle on >= 98 % of
+    images (the fast mode's bar, as at config 4)."""
+    from adaptive_amd import Config, Encoder2Decoder
+    from oracle.adaptive_oracle import BeamOracle
+    cf = Config(vocab_length=3001)
+    m = Encoder2Decoder(cf).to(gpu_device)
+    m.load_synthetic(11)
+    f = synth.make_features(64, seed=8)
+    ids, _, _, seqs, scores = m.beam_search(torch.from_numpy(f).to(gpu_device), 12, 3, fast=True)
+    o = BeamOracle(synth.make_weights(11, m.dims)).beam_search(torch.from_numpy(f), 12, 3)
+    same = (seqs.cpu() == o[3]).all(dim=(1, 2)).float().mean().item()
+    assert same >= 0.98, same
 
 
 def test_beam_batch_invariance(gpu_device):

@@ -131,9 +131,9 @@ def test_config3_b4096_equals_eight_b512_blocks(gpu_device):
     from oracle.adaptive_oracle import OracleModel, top2_margin
     m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
     feats = synthetic_features(4096, gpu_device, seed=0)
-    full = m.sampler(feats, max_len=20, graph=False)
+    full = m.sampler(feats, max_len=20)
     for k in range(8):
-        blk = m.sampler(feats[512 * k: 512 * (k + 1)].contiguous(), max_len=20, graph=False)
+        blk = m.sampler(feats[512 * k: 512 * (k + 1)].contiguous(), max_len=20)
         for a, b in zip(full, blk):
             assert torch.equal(a[512 * k: 512 * (k + 1)], b), k
     rows = [512 * k + o for k in range(8) for o in (0, 137, 300, 511)]
@@ -195,7 +195,7 @@ def test_sharded_sampler_processes_equal_one_process(gpu_device, backend, world,
             p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
     m = Encoder2Decoder(Config()).to(gpu_device).load_synthetic(123)
-    ref = m.sampler(synthetic_features(total, gpu_device, seed=0), max_len=T, graph=False)
+    ref = m.sampler(synthetic_features(total, gpu_device, seed=0), max_len=T)
     for x, r in zip(got, ref + ref):
         assert torch.equal(x, r.cpu())
 

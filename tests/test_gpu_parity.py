@@ -68,23 +68,19 @@ def test_encoder_tail(model, oracle, gpu_device):
 
 @pytest.mark.parametrize("B", [67, 512])
 def test_split_bf16_encoder_is_fp32_accurate(model, oracle, gpu_device, B):
-    """Both bf16x3 encoders (3-way bf16 split on bf16 MFMA: k_enc_v4, the default, and k_enc_v3)
-    vs an fp64 reference: their error is of the same order as the fp32-MFMA encoder's (K = 2048
-    fp32 accumulation), far below the 2e-5 parity tolerance.  B = 67 -> 3283 rows: a ragged last
-    128-row tile (v3) and a last two-image workgroup holding one image (v4); B = 512: the bench grid."""
+    """The bf16x3 encoder (3-way bf16 split on bf16 MFMA: k_enc_v4 + k_gemm3 heads) vs an fp64
+    reference: its error is of the same order as the fp32-MFMA encoder's (k_enc_v + k_enc_heads;
+    K = 2048 fp32 accumulation), far below the 2e-5 parity tolerance.  B = 67 -> 3283 rows: a last
+    two-image workgroup holding one image; B = 512: the bench grid."""
     feats = torch.from_numpy(synth.make_features(B, seed=3)).to(gpu_device)
     out4 = model._encode(feats)
     V4 = out4[0].cpu().numpy().astype(np.float64)
     try:
-        model.enc_v3 = True
-        out3 = model._encode(feats)
-        V3 = out3[0].cpu().numpy().astype(np.float64)
-        model.enc_v3 = False
         model.fp32_encoder = True
-        V1 = model._encode(feats)[0].cpu().numpy().astype(np.float64)
+        out1 = model._encode(feats)
+        V1 = out1[0].cpu().numpy().astype(np.float64)
     finally:
         model.fp32_encoder = False
-        model.enc_v3 = False
     A = feats.cpu().numpy().astype(np.float64).reshape(B, 2048, 49).transpose(0, 2, 1)
     W = oracle.w["encoder.affine_a.weight"].numpy().astype(np.float64)
     b = oracle.w["encoder.affine_a.bias"].numpy().astype(np.float64)
@@ -92,25 +88,24 @@ def test_split_bf16_encoder_is_fp32_accurate(model, oracle, gpu_device, B):
     ref = np.maximum(pre, 0.0)
     scale = np.abs(A) @ np.abs(W).T + np.abs(b)          # sum_k |a_k w_k| + |b| per output
     e1 = np.abs(V1 - ref) / scale
-    for name, Vx in (("k_enc_v4", V4), ("k_enc_v3", V3)):
-        ex = np.abs(Vx - ref) / scale
-        assert ex.max() < 2e-6, (name, ex.max())        # fp32 GEMM class: ~K u / sqrt(K) << 1e-5
-        assert ex.max() < 4 * e1.max() + 1e-7, (name, ex.max(), e1.max())
-        assert np.abs(Vx - ref).max() < ATT_TOL / 2, name
-    # heads: k_enc_heads3 (bf16x3, default) and k_enc_heads (fp32 MFMA, with k_enc_v3) vs fp64
+    e4 = np.abs(V4 - ref) / scale
+    assert e4.max() < 2e-6, e4.max()                     # fp32 GEMM class: ~K u / sqrt(K) << 1e-5
+    assert e4.max() < 4 * e1.max() + 1e-7, (e4.max(), e1.max())
+    assert np.abs(V4 - ref).max() < ATT_TOL / 2
+    # heads: k_gemm3 (bf16x3, default) and k_enc_heads (fp32 MFMA) vs fp64
     a_g = out4[3].cpu().numpy().astype(np.float64)
-    assert np.array_equal(out4[3].cpu().numpy(), out3[3].cpu().numpy()), "fused avg-pool == k_avgpool"
-    for key, act, got4, got3 in (("encoder.affine_b", np.maximum, out4[1], out3[1]),
-                                 ("encoder.affine_h0", np.tanh, out4[2][0][:, 0], out3[2][0][:, 0]),
-                                 ("encoder.affine_c0", np.tanh, out4[2][1][:, 0], out3[2][1][:, 0])):
+    assert np.array_equal(out4[3].cpu().numpy(), out1[3].cpu().numpy()), "fused avg-pool == k_avgpool"
+    for key, act, got4, got1 in (("encoder.affine_b", np.maximum, out4[1], out1[1]),
+                                 ("encoder.affine_h0", np.tanh, out4[2][0][:, 0], out1[2][0][:, 0]),
+                                 ("encoder.affine_c0", np.tanh, out4[2][1][:, 0], out1[2][1][:, 0])):
         Wh = oracle.w[key + ".weight"].numpy().astype(np.float64)
         bh = oracle.w[key + ".bias"].numpy().astype(np.float64)
         pre = a_g @ Wh.T + bh
         r = np.maximum(pre, 0.0) if act is np.maximum else np.tanh(pre)
         sc = np.abs(a_g) @ np.abs(Wh).T + np.abs(bh)
         e4 = np.abs(got4.cpu().numpy() - r) / sc
-        e3 = np.abs(got3.cpu().numpy() - r) / sc
-        assert e4.max() < 2e-6 and e4.max() < 4 * e3.max() + 1e-7, (key, e4.max(), e3.max())
+        e1 = np.abs(got1.cpu().numpy() - r) / sc
+        assert e4.max() < 2e-6 and e4.max() < 4 * e1.max() + 1e-7, (key, e4.max(), e1.max())
 
 
 def test_decode_step_logits(model, oracle, gpu_device):
@@ -178,69 +173,44 @@ def test_batch_invariance(model, gpu_device):
         assert torch.equal(b2, beta[lo:hi])
 
 
-@pytest.mark.parametrize("lanes,B,exact", [(2, 512, False), (3, 300, False), (4, 200, True), (8, 100, False)])
-def test_lanes_equal_single_stream(model, gpu_device, lanes, B, exact):
-    """Splitting the step loop over HIP streams by row blocks changes nothing, bitwise."""
-    feats = torch.from_numpy(synth.make_features(B, seed=13)).to(gpu_device)
-    ref = model.sampler(feats, max_len=9, exact_vocab=exact, lanes=1)
-    got = model.sampler(feats, max_len=9, exact_vocab=exact, lanes=lanes)
-    torch.cuda.synchronize()
-    for r, g in zip(ref, got):
-        assert torch.equal(r, g)
-
-
-@pytest.mark.parametrize("lanes,exact", [(1, False), (2, False), (1, True), (4, True)])
-def test_graph_plan_replay_equals_direct(model, gpu_device, lanes, exact):
-    """Captured decode plans (hipGraph) give the direct path's results, also after the input buffer
-    is overwritten in place (the plan reads its buffer at every launch)."""
+@pytest.mark.parametrize("exact", [False, True])
+def test_decode_plan_replay_equals_sampler(model, gpu_device, exact):
+    """A DecodePlan (the whole decode captured once into a hipGraph over buffers the plan owns) gives
+    sampler's results bit for bit, for every batch copied into it -- including batches held in
+    freshly allocated tensors -- and keeps nothing of the caller's."""
+    import weakref
+    from adaptive_amd import DecodePlan
     B = 192
-    feats = torch.from_numpy(synth.make_features(B, seed=17)).to(gpu_device)
-    ref = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=False)
-    for _ in range(3):  # 1st: direct, 2nd: capture + launch, 3rd: replay
-        got = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=True)
+    plan = DecodePlan(model, B, max_len=7, exact_vocab=exact)
+    for seed in (17, 18, 17):
+        feats = torch.from_numpy(synth.make_features(B, seed=seed)).to(gpu_device)
+        ref = model.sampler(feats, max_len=7, exact_vocab=exact)
+        got = plan(feats)
         for r, g in zip(ref, got):
             assert torch.equal(r, g)
-    feats.copy_(torch.from_numpy(synth.make_features(B, seed=18)).to(gpu_device))
-    ref2 = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=False)
-    got2 = model.sampler(feats, max_len=7, exact_vocab=exact, lanes=lanes, graph=True)
-    for r, g in zip(ref2, got2):
-        assert torch.equal(r, g)
-    assert not torch.equal(ref[0], ref2[0])
+        w = weakref.ref(feats)
+        del feats, got
+        assert w() is None, "DecodePlan retained the caller's batch"
+    plan.close()
 
 
-@pytest.mark.parametrize("B,exact,graph", [(512, False, False), (77, False, False), (130, True, False),
-                                           (512, False, True), (77, False, True)])
-def test_split_lstm_step_equals_fused(model, gpu_device, B, exact, graph):
-    """The split LSTM step (k_lstm_gemm of step t+1 on the side stream beside step t's attention and
-    vocab stages, then k_lstm_cell) gives the one-launch k_lstm's results bit for bit, direct and
-    captured (graph: first call direct, second capture + launch, third replay)."""
-    feats = torch.from_numpy(synth.make_features(B, seed=31)).to(gpu_device)
-    ref = model.sampler(feats, max_len=11, exact_vocab=exact, graph=False)
-    model.split_lstm = True
-    try:
-        for _ in range(3 if graph else 1):
-            got = model.sampler(feats, max_len=11, exact_vocab=exact, graph=graph)
-            torch.cuda.synchronize()
-            for r, g in zip(ref, got):
-                assert torch.equal(r, g)
-    finally:
-        model.split_lstm = False
-
-
-@pytest.mark.parametrize("B", [512, 300, 77, 4])
-def test_wide_screen_equals_screen64(model, gpu_device, B):
-    """The 128 x 160-tile screen (k_vscreen2) and the 64 x 64-tile one (k_vscreen) bound the same
-    logits: the decode's ids / alpha / beta are identical (the exact rescoring decides the ids)."""
-    feats = torch.from_numpy(synth.make_features(B, seed=41)).to(gpu_device)
-    got = model.sampler(feats, max_len=12, graph=False)
-    model.screen64 = True
-    try:
-        ref = model.sampler(feats, max_len=12, graph=False)
-    finally:
-        model.screen64 = False
-    torch.cuda.synchronize()
-    for r, g in zip(ref, got):
-        assert torch.equal(r, g)
+@pytest.mark.parametrize("hidden,B", [(256, 37), (768, 20)])
+def test_other_hidden_sizes_vs_oracle(gpu_device, hidden, B):
+    """The general-dims kernels: hidden 256 (k_vscreen2 tiles, k_enc_v4<2>) and 768 (the 64 x 64
+    screen k_vscreen, the 128 x 128-tile encoder k_enc_v3, k_atten<3>) against the oracle."""
+    from adaptive_amd import Config, Encoder2Decoder
+    from oracle.adaptive_oracle import OracleModel
+    cf = Config(adaptive_word_embed_size=256, adaptive_lstm_hidden_size=hidden, vocab_length=3001)
+    m = Encoder2Decoder(cf).to(gpu_device)
+    m.load_synthetic(7)
+    feats = synth.make_features(B, seed=29)
+    ids, alpha, beta = m.sampler(torch.from_numpy(feats).to(gpu_device), max_len=12)
+    r_ids, r_alpha, r_beta = OracleModel(synth.make_weights(7, m.dims)).sampler(torch.from_numpy(feats), max_len=12)
+    assert torch.equal(ids.cpu(), r_ids)
+    np.testing.assert_allclose(alpha.cpu().numpy(), r_alpha.numpy(), atol=ATT_TOL, rtol=0)
+    np.testing.assert_allclose(beta.cpu().numpy(), r_beta.numpy(), atol=ATT_TOL, rtol=0)
+    ex = m.sampler(torch.from_numpy(feats).to(gpu_device), max_len=12, exact_vocab=True)
+    assert torch.equal(ex[0].cpu(), r_ids)
 
 
 def test_greedy_matches_oracle_odd_batch(model, oracle, gpu_device):
@@ -329,34 +299,16 @@ def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device)
     assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
 
 
-@pytest.mark.parametrize("B,lanes", [(512, 1), (300, 1), (77, 1), (4, 1), (512, 2)])
-def test_vocab_lists_equal_summaries(model, gpu_device, B, lanes):
-    """k_vscreen3 + k_vrescore3 (per-row candidate lists decided against the running max lower bound)
-    == k_vscreen2 + k_vrescore (granule summaries): ids, alpha, beta identical."""
-    feats = torch.from_numpy(synth.make_features(B, seed=43)).to(gpu_device)
-    ref = model.sampler(feats, max_len=13, graph=False, lanes=lanes)
-    model.vocab_lists = True
-    try:
-        got = model.sampler(feats, max_len=13, graph=False, lanes=lanes)
-    finally:
-        model.vocab_lists = False
-    torch.cuda.synchronize()
-    for r, g in zip(ref, got):
-        assert torch.equal(r, g)
-
-
-@pytest.mark.parametrize("lists", [False, True])
-def test_all_columns_tied_rescore_overflow(gpu_device, lists):
-    """W_m = 0, b_m = 0: every logit is exactly 0, so every column is a candidate (k_vscreen3's
-    per-row lists and k_vrescore's candidate list overflow into their all-columns fallbacks).  The
-    first index (0) must win everywhere, as torch's max(2)[1]."""
+def test_all_columns_tied_rescore_overflow(gpu_device):
+    """W_m = 0, b_m = 0: every logit is exactly 0, so every column is a candidate (k_vrescore's
+    candidate list overflows into its all-columns fallback).  The first index (0) must win
+    everywhere, as torch's max(2)[1]."""
     m = _model()
     with torch.no_grad():
         m.decoder.adaptive.mlp.weight.zero_()
         m.decoder.adaptive.mlp.bias.zero_()
-    m.vocab_lists = lists
     feats = torch.from_numpy(synth.make_features(130, seed=4)).to(gpu_device)
-    ids, _, _ = m.sampler(feats, max_len=3, graph=False)
+    ids, _, _ = m.sampler(feats, max_len=3)
     assert torch.equal(ids, torch.zeros_like(ids))
-    ex, _, _ = m.sampler(feats, max_len=3, graph=False, exact_vocab=True)
+    ex, _, _ = m.sampler(feats, max_len=3, exact_vocab=True)
     assert torch.equal(ex, ids)

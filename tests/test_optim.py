@@ -63,5 +63,9 @@ def test_capi_argument_errors(lib):
     assert lib.aa_cross_entropy_forward(256, 4, 10, 9, 256, -100, 256, 256, 256, 48, None) == -3  # ldx < V
     assert lib.aa_cross_entropy_forward(256, 4, 10, 10, None, -100, 256, 256, 256, 48, None) == -1
     assert lib.aa_cross_entropy_forward(256, 4, 10, 10, 256, -100, 256, 256, 256, 47, None) == -4
-    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, None, 10, None) == -1
-    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, 256, 8, None) == -3
+    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, 48, None, 10, None) == -1
+    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, 48, 512, 8, None) == -3
+    # a workspace from a forward over fewer rows is refused
+    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, 47, 512, 10, None) == -4
+    # in place (dlogits == logits) only with the same pitch
+    assert lib.aa_cross_entropy_backward(256, 4, 10, 10, 256, -100, 256, 256, 256, 48, 256, 12, None) == -3

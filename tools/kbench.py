@@ -16,7 +16,7 @@ SO = os.path.join(ROOT, "tools", "_build", "libkbench.so")
 
 
 def main():
-    names = sys.argv[1:] or ["lstm", "atten", "vscreen", "vrescore", "enc_v3"]
+    names = sys.argv[1:] or ["lstm", "atten", "vscreen", "vrescore"]
     if not os.path.exists(SO):
         os.makedirs(os.path.dirname(SO), exist_ok=True)
         subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
@@ -26,7 +26,7 @@ def main():
     model = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
     B, T = 512, 20
     feats = synthetic_features(B, dev, seed=0)
-    model.sampler(feats, max_len=T, graph=False)
+    model.sampler(feats, max_len=T)
     torch.cuda.synchronize()
     libs = {}
     for key, path in (("", SO), ("old:", os.environ.get("KB_SO_OLD", ""))):  # "old:<name>" -> a second build

@@ -31,13 +31,12 @@ def main():
     lib.aa_ts_setup.argtypes = [ctypes.c_void_p]
     buf = torch.zeros(5 * 2048 * 16, dtype=torch.int64, device=dev)
     m = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
-    m.vocab_lists = bool(os.environ.get("AA_VOCAB_LISTS"))
     feats = synthetic_features(512, dev, seed=0)
     for rep in range(3):
         buf.zero_()
         torch.cuda.synchronize()
         _lib.check(lib.aa_ts_setup(buf.data_ptr()), "ts_setup")
-        m.sampler(feats, max_len=20, graph=False)
+        m.sampler(feats, max_len=20)
         torch.cuda.synchronize()
     ts = buf.view(5, 2048, 16).cpu().numpy()
     for kid, (name, marks) in KERNELS.items():
