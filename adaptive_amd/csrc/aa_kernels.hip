@@ -601,6 +601,189 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
 }
 
 // ---------------------------------------------------------------------------------------------
+// E1' (k_enc_v5, the default at H = 512 / 256): k_enc_v4's workgroup (two images, all H columns),
+// MFMA order and epilogue -- bit-identical V -- restructured around the LDS:
+//  * 64-channel stages (two 32-channel chunks) instead of 32: half the barriers (32 per workgroup),
+//    and a stage's loads get two chunks of MFMA work to land behind;
+//  * no fp32 stage copy for the avg-pool: every fp32 x is exactly h + m + l of its three bf16
+//    planes (RNE split: x - h has <= 16 significant bits, its remainder after m <= 8), and
+//    ((float)h + (float)m) + (float)l reproduces it exactly, so one wave per stage rebuilds each
+//    channel's 49 values from the A planes already in LDS and sums them in p order (k_avgpool's
+//    arithmetic, bit-identical a_g, written straight to memory: no a_g array in LDS either);
+//  * staging stores without bank conflicts: a ds_write_b128 is serviced in groups of 8 contiguous
+//    lanes on 32 banks, and 8 consecutive rows at the 96-B pitch (6 16-B slots) hit only 4 distinct
+//    slots; each group of 8 lanes now takes 4 rows x 2 channel groups: slots (6 j + k) mod 8, j < 4,
+//    k < 2, are all distinct.  The 96-B pitch stays (conflict-free ds_read_b128 fragment reads);
+//  * every wave stages (800 staging lanes: 25 four-row blocks x 2 chunks x 2 channel-group pairs).
+// LDS: [2 buffers][2 chunks][3 planes][112 rows][48] bf16, each chunk's planes 64 B apart from the
+// other's (the avg-pool's dword reads of the two chunks land on different banks) = 126 KB.
+// ---------------------------------------------------------------------------------------------
+constexpr int E5_PL = 7 * 16 * E4_LD;           // one plane of one chunk (bf16)
+constexpr int E5_CH = 3 * E5_PL + 32;           // one chunk: 3 planes + 64 B
+constexpr int E5_BUF = 2 * E5_CH;               // one 64-channel stage
+constexpr int E5_TASKS = 25 * 2 * 2 * 8;        // staging lanes (rows 98, 99 clamp to valid rows, never stored)
+template <int NCB, int NW>
+__global__ __launch_bounds__(64 * NW) void k_enc_v5(const float* __restrict__ feats, int B, int C,
+                                                const bf16x8* __restrict__ W4, const float* __restrict__ bias,
+                                                float* __restrict__ V, float* __restrict__ a_g) {
+  static_assert(NCB % 2 == 0, "columns are processed in pairs of 16-column blocks");
+  constexpr int H = 16 * NCB * NW, NPAIR = NCB / 2;
+  constexpr int NT = 64 * NW, ST = (E5_TASKS + NT - 1) / NT;  // staging tasks per thread
+  __shared__ __attribute__((aligned(16))) __bf16 As[2 * E5_BUF];
+  const int M = B * P, KC = C / 32, NS = C / 64;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = blockIdx.x * E4_ROWS;
+  // staging task q (lane group g8 = q >> 3, i = q & 7): rows 4 rb + (i & 3) of four-row block rb =
+  // g8 % 25, chunk hp >> 1 and channel group 2 (hp & 1) + (i >> 2) (8 channels) of it, hp = g8 / 25
+  const float* src[ST];
+  int so[ST];
+  bool act[ST];
+#pragma unroll
+  for (int j = 0; j < ST; ++j) {
+    const int q = t + j * NT;
+    act[j] = q < E5_TASKS;
+    const int g8 = act[j] ? q >> 3 : 0, i = q & 7;
+    const int rb = g8 % 25, hp = g8 / 25, ch = hp >> 1, kg = 2 * (hp & 1) + (i >> 2);
+    const int r = 4 * rb + (i & 3);
+    int m = m0 + (r < E4_ROWS ? r : E4_ROWS - 1);
+    m = m < M ? m : M - 1;  // clamp, never zero (rows >= M and r >= 98 are not stored)
+    const int bi = m / P, pi = m - bi * P;
+    src[j] = feats + (int64_t)bi * C * P + pi + (int64_t)(32 * ch + 8 * kg) * P;
+    so[j] = ch * E5_CH + r * E4_LD + 8 * kg;
+  }
+  const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);  // fragment reads: row 16 rb + (l & 15), k 8 (l >> 4)
+  const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;
+  float ra[ST][8];
+  bf16x8 wv[NCB][3];
+  floatx4 acc[E4_RB][NCB];
+#pragma unroll
+  for (int rb = 0; rb < E4_RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto gload_a = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j)
+      if (act[j]) {
+        const float* sp = src[j] + (int64_t)(64 * s) * P;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ra[j][i] = AA_FEAT_LOAD(sp + i * P);
+      }
+  };
+  auto gload_w = [&](int kc, int c) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)kc * 3 + q) * 64];
+  };
+  auto lstore_a = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j)
+      if (act[j]) {
+        bf16x8 x[3];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __bf16 x0, x1, x2;
+          split3(ra[j][i], x0, x1, x2);
+          x[0][i] = x0; x[1][i] = x1; x[2][i] = x2;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&As[buf * E5_BUF + so[j] + q * E5_PL]) = x[q];
+      }
+  };
+  gload_a(0);
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) gload_w(0, c);
+  lstore_a(0);
+  gload_a(NS > 1 ? 1 : 0);
+  __syncthreads();
+  for (int s = 0; s < NS; ++s) {
+    const int buf = s & 1, s2 = s + 2 < NS ? s + 2 : NS - 1;
+    // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
+    lstore_a(buf ^ 1);
+    gload_a(s2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kc = 2 * s + h, kn = kc + 1 < KC ? kc + 1 : KC - 1;
+      const __bf16* Ab = &As[buf * E5_BUF + h * E5_CH + fo];
+#pragma unroll
+      for (int cp = 0; cp < NPAIR; ++cp) {
+#pragma unroll
+        for (int rb = 0; rb < E4_RB; ++rb) {
+          bf16x8 fa[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(Ab + q * E5_PL + rb * 16 * E4_LD);
+          const int c0 = 2 * cp, c1 = c0 + 1;
+          floatx4 x = acc[rb][c0], y = acc[rb][c1];
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c1][0], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][1], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][1], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][2], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][2], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][0], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][1], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][1], y, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][0], x, 0, 0, 0);
+          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][0], y, 0, 0, 0);
+          acc[rb][c0] = x;
+          acc[rb][c1] = y;
+        }
+        gload_w(kn, 2 * cp);
+        gload_w(kn, 2 * cp + 1);
+        asm volatile("" ::: "memory");
+      }
+    }
+    // one wave per stage (rotating) rebuilds the stage's 2 images x 64 channels from the three planes
+    // and sums them in p order: lane -> image lane >> 5, channels 2 (lane & 31), + 1 (chunk (lane >> 4) & 1)
+    if (wave == (s % NW)) {
+      const int img = lane >> 5, cpair = lane & 31, ch = cpair >> 4, cl = 2 * (cpair & 15);
+      const __bf16* pb = &As[buf * E5_BUF + ch * E5_CH + (img * P) * E4_LD + cl];
+      float s0 = 0.f, s1 = 0.f;
+      for (int pp = 0; pp < P; ++pp) {
+        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD);
+        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD + E5_PL);
+        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD + 2 * E5_PL);
+        s0 += (__uint_as_float(w0 << 16) + __uint_as_float(w1 << 16)) + __uint_as_float(w2 << 16);
+        s1 += (__uint_as_float(w0 & 0xFFFF0000u) + __uint_as_float(w1 & 0xFFFF0000u)) + __uint_as_float(w2 & 0xFFFF0000u);
+      }
+      const int b = 2 * blockIdx.x + img;
+      if (b < B) {
+        float* dst = a_g + (int64_t)b * C + 64 * s + 32 * ch + cl;
+        dst[0] = s0 / 49.0f;
+        dst[1] = s1 / 49.0f;
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // epilogue (as k_enc_v4): each 16-row block through LDS, out as whole contiguous rows of V
+  float* Vs = reinterpret_cast<float*>(&As[0]);
+  constexpr int VSP = H + 4;
+  static_assert(16 * VSP * 4 <= sizeof(As), "V staging must fit in the A stages");
+  float bvs[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) bvs[c] = bias[(wave * NCB + c) * 16 + (lane & 15)];
+#pragma unroll
+  for (int rb = 0; rb < E4_RB; ++rb) {
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const int col = (wave * NCB + c) * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Vs[(4 * (lane >> 4) + i) * VSP + col] = reluf_(acc[rb][c][i] + bvs[c]);
+    }
+    __syncthreads();
+    constexpr int F4 = 16 * H / 4;
+#pragma unroll
+    for (int q = t; q < F4; q += NT) {
+      const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
+      if (tr < E4_ROWS && row < M)
+        *reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4) = *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // E2: heads.  [v_g | h0 | c0] = a_g · [W_b; W_h0; W_c0]^T + b, relu / tanh / tanh by column.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_enc_heads(const float* __restrict__ a_g, int B, int C, int E, int H, int NHp,
@@ -1064,7 +1247,8 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
   // the tile's 64 tokens by ONE LDS-DMA of wave 0 (the low dword of each int64 token), so that no
   // ordinary load is outstanding beside the ring's DMAs: hipcc drains every DMA (vmcnt(0)) before
   // the first use of an ordinary load's result while a DMA is in flight
-  if (t < 64) {
+  // (tok == nullptr: the first step of a greedy decode, every row starts from <start> = 1: no load)
+  if (t < 64 && tok) {
     const int r = m0 + t < B ? m0 + t : B - 1;
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tok + (int64_t)r * tok_ld),
                                      (__attribute__((address_space(3))) void*)tok_lds, 4, 0, 0);
@@ -1113,7 +1297,7 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
     // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
     if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    tk = tok_lds[rr];
+    tk = tok ? tok_lds[rr] : 1;
     gathers();
     asm volatile("" ::: "memory");
   });
@@ -2483,16 +2667,27 @@ static bool enc_v4(const Layout& L, int32_t flags) {
 static bool gemm3_ok(int32_t flags, int K) {
   return !(flags & AA_DECODE_FP32_ENCODER) && K % 256 == 0;
 }
+// k_enc_v5 (64-channel stages) unless AA_ENC_V4=1 (A/B of the two encoders; bit-identical outputs)
+static bool enc_v5() {
+  static const bool v = [] {
+    const char* e = getenv("AA_ENC_V4");
+    return !(e && atoi(e) == 1);
+  }();
+  return v;
+}
+// hsp0 != nullptr (greedy decode): h0 split into the 3-plane fragments k_lstm reads, on `s` after the
+// VWv GEMM, waiting for the heads only (the aux stream's x_g GEMM is still running: off the critical path)
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
-                          hipStream_t s, hipStream_t aux = nullptr) {
+                          hipStream_t s, hipStream_t aux = nullptr, bf16x8* hsp0 = nullptr) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, heads_done = nullptr;
   hipStream_t sa = s;
   if (aux && aux != s) {
     AA_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
     AA_TRY(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    if (hsp0) AA_TRY(hipEventCreateWithFlags(&heads_done, hipEventDisableTiming));
     AA_TRY(hipEventRecord(fork, s));
     AA_TRY(hipStreamWaitEvent(aux, fork, 0));
     sa = aux;
@@ -2512,6 +2707,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
                          B, C, NH, p.heads_w4, p.heads_b, v_g, 0, h0, c0, E, H);
     }
     rec(ev, 5, st);
+    if (heads_done) (void)hipEventRecord(heads_done, st);
     rec(ev, 8, st);
     if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0)
       hipLaunchKernelGGL((k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st, v_g, B, E,
@@ -2528,11 +2724,17 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     rec(ev, 1, s);
     rec(ev, 2, s);
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
-    if (H == 512)
+    if (enc_v5()) {
+      if (H == 512)
+        hipLaunchKernelGGL((k_enc_v5<2, 16>), dim3(nwg), dim3(1024), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+      else
+        hipLaunchKernelGGL((k_enc_v5<2, 8>), dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+    } else if (H == 512) {
       hipLaunchKernelGGL((k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg),
                          dim3(64 * AA_ENC4_NW), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-    else
+    } else {
       hipLaunchKernelGGL(k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+    }
     rec(ev, 3, s);
     if (sa != s) {  // aux waits for a_g
       hipEvent_t agr = nullptr;
@@ -2564,6 +2766,12 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
   else if (VWv)
     gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
   rec(ev, 7, s);
+  if (hsp0) {
+    if (heads_done) AA_TRY(hipStreamWaitEvent(s, heads_done, 0));
+    hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (H / 8) + 255) / 256)), dim3(256), 0, s, h0, B, H,
+                       hsp0);
+  }
+  if (heads_done) AA_TRY(hipEventDestroy(heads_done));
   if (join) {
     AA_TRY(hipEventRecord(join, sa));
     AA_TRY(hipStreamWaitEvent(s, join, 0));
@@ -2800,8 +3008,8 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   const bool wide = screen_wide(L);
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
-    // token of step t-1: ids[:, t-1] (written by the previous step), <start> at t = 0
-    const int64_t* tok = t ? ids + (t - 1) : w.tok0;
+    // token of step t-1: ids[:, t-1] (written by the previous step); t = 0: nullptr = <start> for every row
+    const int64_t* tok = t ? ids + (t - 1) : nullptr;
     const int tok_ld = t ? T : 1;
     uint64_t* kt = w.keys + (size_t)t * B;
     float* alt = alpha ? alpha + (size_t)t * P : nullptr;
@@ -2869,18 +3077,14 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
-                      trace ? trace->encoder_events : nullptr, flags, s, aux);
+                      trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0]);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (L.H / 8) + 255) / 256)), dim3(256), 0, s, w.h[0], B,
-                     L.H, w.hsp[0]);
-  {
+  if (flags & AA_DECODE_EXACT_VOCAB) {
     // the exact vocab stage accumulates into keys by atomicMax (k_vocab); the default stage writes
-    // every key it produces, so it needs no clearing
-    const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
-    const int n = exact ? T * B : 0, nb = n > B ? n : B;
-    const int nblk = nb / 256 + 1;
-    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1,
-                       exact ? w.keys : nullptr, n);
+    // every key it produces, so it needs no clearing (and step 0's k_lstm takes <start> itself)
+    const int n = T * B, nblk = n / 256 + 1;
+    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1, w.keys,
+                       n);
   }
   return decode_rows(L, p, w, B, T, flags, ids, alpha, beta, trace, s);
 }

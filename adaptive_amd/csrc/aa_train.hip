@@ -948,6 +948,167 @@ __global__ void k_tr_cell_bwd_sk(const float* __restrict__ dH, const float* __re
   dc_rec[i] = dc * f_;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused recurrent LSTM steps (bf16 steps): ONE launch per timestep, forward and backward through
+// time, in place of a split-K k_tgemm<true> of h_{t-1} W_hh^T (or DG_{t+1} W_hh) plus a cell kernel
+// that sums its partials (k_tr_cell_sk / k_tr_cell_bwd_sk: two launches and a partial-slab round
+// trip per step).  A workgroup owns 16 rows and 16 hidden units (all four gates of them, so the
+// cell runs in its epilogue); the grid is ceil(B/16) x H/16 workgroups, unit group fastest, so the
+// workgroups that read one W slice share an XCD.  The GEMM runs on v_mfma_f32_16x16x32_bf16 (bf16
+// operands, RNE -- the rounding k_tgemm<true> applies while staging -- and fp32 accumulation) with K
+// split over the 4 waves; every operand fragment is loaded straight into registers (16 B per lane,
+// all of a wave's loads issued together: a step is a few dependent round trips, not a byte budget),
+// and the 4 partial tiles are summed in LDS in a fixed order ((w0 + w1) + (w2 + w3)): deterministic.
+// Operands come pre-packed: W_hh once per call as 16x16x32 B-fragments (k_pk_whh), h_t / DG_t as
+// bf16 row copies written by the previous step's epilogue (the fp32 ones stay for the weight
+// gradients).  The persistent alternative (W_hh resident in LDS across all T steps, a grid barrier
+// per step) was priced and not built: DESIGN.md §9.
+// ---------------------------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// W_hh [4H][H] fp32 -> bf16 16x16x32 B-fragments (lane l, element e).  mode 0 (forward, gates):
+// whf[ug][g][kc][l][e] = W_hh[g H + 16 ug + (l & 15)][32 kc + 8 (l >> 4) + e]; mode 1 (backward,
+// W_hh^T): whb[ug][kc][l][e] = W_hh[32 kc + 8 (l >> 4) + e][16 ug + (l & 15)], kc < 4H / 32.
+__global__ void k_pk_whh(const float* __restrict__ w, int H, int mode, bf16x8* __restrict__ out) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= (int64_t)4 * H * H / 8) return;
+  const int l = (int)(f & 63);
+  const int64_t q = f >> 6;
+  bf16x8 v;
+  if (mode == 0) {
+    const int KC = H / 32, kc = (int)(q % KC), g = (int)((q / KC) % 4), ug = (int)(q / (4 * KC));
+    const float* src = w + (int64_t)(g * H + 16 * ug + (l & 15)) * H + 32 * kc + 8 * (l >> 4);
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    v[0] = (__bf16)a.x; v[1] = (__bf16)a.y; v[2] = (__bf16)a.z; v[3] = (__bf16)a.w;
+    v[4] = (__bf16)b.x; v[5] = (__bf16)b.y; v[6] = (__bf16)b.z; v[7] = (__bf16)b.w;
+  } else {
+    const int KC4 = 4 * H / 32, kc = (int)(q % KC4), ug = (int)(q / KC4);
+    const float* src = w + (int64_t)(32 * kc + 8 * (l >> 4)) * H + 16 * ug + (l & 15);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)src[(int64_t)e * H];
+  }
+  out[f] = v;
+}
+
+// Forward step t: gates = h_{t-1} W_hh^T + PRE[t] (x W_ih^T + b_ih + b_hh), then the cell exactly as
+// k_tr_cell_sk (same expression order), writing h, c, the activated gates GA and h in bf16 (the
+// next step's operand).  AF32: h_{t-1} is fp32 (t = 0: h0 from the encoder), else bf16.
+template <int H, bool AF32>
+__global__ __launch_bounds__(256) void k_tr_lstm_f(int B, const void* __restrict__ hprev, const float* __restrict__ PRE,
+                                                   int ldp, const float* __restrict__ c_prev,
+                                                   const bf16x8* __restrict__ whf, float* __restrict__ h_out,
+                                                   float* __restrict__ c_out, float* __restrict__ GA,
+                                                   __bf16* __restrict__ hb_out) {
+  constexpr int NUG = H / 16, KC = H / 32, PER = KC / 4;
+  __shared__ float red[4][4][16][17];  // [wave][gate][row][unit]
+  const int ug = blockIdx.x % NUG, m0 = (blockIdx.x / NUG) * 16;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int kc0 = w * PER;
+  const int arow = m0 + (lane & 15) < B ? m0 + (lane & 15) : B - 1;
+  bf16x8 fw[4][PER], fa[PER];
+  const bf16x8* ws = whf + (size_t)ug * 4 * KC * 64 + lane;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) fw[g][i] = ws[((size_t)g * KC + kc0 + i) * 64];
+  if constexpr (AF32) {
+    const float* hp = static_cast<const float*>(hprev) + (int64_t)arow * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const float4 a = *reinterpret_cast<const float4*>(hp + 32 * (kc0 + i));
+      const float4 b = *reinterpret_cast<const float4*>(hp + 32 * (kc0 + i) + 4);
+      fa[i][0] = (__bf16)a.x; fa[i][1] = (__bf16)a.y; fa[i][2] = (__bf16)a.z; fa[i][3] = (__bf16)a.w;
+      fa[i][4] = (__bf16)b.x; fa[i][5] = (__bf16)b.y; fa[i][6] = (__bf16)b.z; fa[i][7] = (__bf16)b.w;
+    }
+  } else {
+    const __bf16* hp = static_cast<const __bf16*>(hprev) + (int64_t)arow * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(hp + 32 * (kc0 + i));
+  }
+  floatx4 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fw[g][i], acc[g], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[w][g][4 * (lane >> 4) + i][lane & 15] = acc[g][i];
+  __syncthreads();
+  const int r = t >> 4, u = t & 15, m = m0 + r;
+  if (m >= B) return;
+  float G[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) G[g] = (red[0][g][r][u] + red[1][g][r][u]) + (red[2][g][r][u] + red[3][g][r][u]);
+  const int j = 16 * ug + u;
+  const float* p = PRE + (int64_t)m * ldp;
+  const float gi = G[0] + p[j], gf = G[1] + p[H + j], gg = G[2] + p[2 * H + j], go = G[3] + p[3 * H + j];
+  const float i_ = sigmoidf_(gi), f_ = sigmoidf_(gf), g_ = tanhf(gg), o_ = sigmoidf_(go);
+  const int64_t i = (int64_t)m * H + j;
+  const float c = f_ * c_prev[i] + i_ * g_;
+  const float h = o_ * tanhf(c);
+  c_out[i] = c;
+  h_out[i] = h;
+  hb_out[i] = (__bf16)h;
+  float* ga = GA + (int64_t)m * 4 * H;
+  ga[j] = i_; ga[H + j] = f_; ga[2 * H + j] = g_; ga[3 * H + j] = o_;
+}
+
+// Backward step t (reverse order): dh_rec = DG_{t+1} W_hh for the workgroup's 16 rows x 16 units (K =
+// 4H over the 4 waves; LAST: t = T - 1, no later step, dh_rec = 0 and no GEMM), then the cell
+// backward exactly as k_tr_cell_bwd_sk, writing DG_t (fp32, for the weight gradients, and bf16, the
+// next backward step's operand) and dc_rec <- dc f.
+template <int H, bool LAST>
+__global__ __launch_bounds__(256) void k_tr_lstm_b(int B, const __bf16* __restrict__ dgb_next,
+                                                   const bf16x8* __restrict__ whb, const float* __restrict__ dH,
+                                                   const float* __restrict__ dC, float* __restrict__ dc_rec,
+                                                   const float* __restrict__ GA, const float* __restrict__ c_t,
+                                                   const float* __restrict__ c_prev, float* __restrict__ DG,
+                                                   __bf16* __restrict__ dgb_out) {
+  constexpr int NUG = H / 16, KC = 4 * H / 32, PER = KC / 4;
+  __shared__ float red[4][16][17];  // [wave][row][unit]
+  const int ug = blockIdx.x % NUG, m0 = (blockIdx.x / NUG) * 16;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if constexpr (!LAST) {
+    const int kc0 = w * PER;
+    const int arow = m0 + (lane & 15) < B ? m0 + (lane & 15) : B - 1;
+    bf16x8 fw[PER], fa[PER];
+    const bf16x8* ws = whb + ((size_t)ug * KC + kc0) * 64 + lane;
+    const __bf16* ap = dgb_next + (int64_t)arow * 4 * H + 8 * (lane >> 4) + 32 * kc0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      fw[i] = ws[(size_t)i * 64];
+      fa[i] = *reinterpret_cast<const bf16x8*>(ap + 32 * i);
+    }
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < PER; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fw[i], acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[w][4 * (lane >> 4) + i][lane & 15] = acc[i];
+    __syncthreads();
+  }
+  const int r = t >> 4, u = t & 15, m = m0 + r;
+  if (m >= B) return;
+  const float dhr = LAST ? 0.f : (red[0][r][u] + red[1][r][u]) + (red[2][r][u] + red[3][r][u]);
+  const int j = 16 * ug + u;
+  const int64_t i = (int64_t)m * H + j;
+  const float* ga = GA + (int64_t)m * 4 * H;
+  const float i_ = ga[j], f_ = ga[H + j], g_ = ga[2 * H + j], o_ = ga[3 * H + j];
+  const float c = c_t[i], tc = tanhf(c);
+  const float dh = dH[i] + dhr;
+  float dc = dC[i] + dc_rec[i] + dh * o_ * (1.f - tc * tc);
+  const float d_o = dh * tc;
+  const float d_i = dc * g_, d_g = dc * i_, d_f = dc * c_prev[i];
+  const float v0 = d_i * i_ * (1.f - i_), v1 = d_f * f_ * (1.f - f_), v2 = d_g * (1.f - g_ * g_), v3 = d_o * o_ * (1.f - o_);
+  float* dg = DG + (int64_t)m * 4 * H;
+  dg[j] = v0; dg[H + j] = v1; dg[2 * H + j] = v2; dg[3 * H + j] = v3;
+  __bf16* db = dgb_out + (int64_t)m * 4 * H;
+  db[j] = (__bf16)v0; db[H + j] = (__bf16)v1; db[2 * H + j] = (__bf16)v2; db[3 * H + j] = (__bf16)v3;
+  dc_rec[i] = dc * f_;
+}
+
 // embedding gradient dE[v] = sum over rows r (t-major) with tok(r) == v of dX[r][0:E], in r order:
 // k_tok_rank: rank of r among the earlier rows with its token (and the token's count via the
 // first occurrence); k_tok_place: position in a token-sorted list; k_tr_embed_bwd: one
@@ -1075,6 +1236,9 @@ struct TrainWS {
   // bf16 operands of the large GEMMs (AA_TRAIN_BF16, k_bgemm): U_p, W_m, dS (rows), W_m^T, dS^T, U_p^T,
   // dV^T, the feature map as [C][B 49]
   __bf16 *ub, *wmb, *dspb, *wmT, *dspT, *upT, *dvT, *ftT;
+  // fused recurrent steps (bf16): W_hh as forward / backward B-fragments, h_t and DG_t ping-pong bf16 copies
+  bf16x8 *whf, *whb;
+  __bf16 *hb[2], *dgb[2];
   int *trank, *tcount, *torder, *tsmall;
 };
 
@@ -1151,6 +1315,12 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
     w.upT = c.take<__bf16>(H * Kr);
     w.dvT = c.take<__bf16>(H * Kb);
     w.ftT = c.take<__bf16>(Cc * Kb);
+    w.whf = c.take<bf16x8>(4 * H * H / 8);
+    w.whb = c.take<bf16x8>(4 * H * H / 8);
+    for (int i = 0; i < 2; ++i) {
+      w.hb[i] = c.take<__bf16>((size_t)B * H);
+      w.dgb[i] = c.take<__bf16>((size_t)B * 4 * H);
+    }
   }
   *bytes = c.off;
   return w;
@@ -1187,14 +1357,39 @@ static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const Train
   tgemm(gc, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
   tgemm(gc, R, H, 2 * E, s.X, 2 * E, 0, w->sent_affine_x_w, 2 * E, 0, s.PRE + 4 * H, 5 * H);
   // LSTM over T steps (baseline_attention.py:167-178)
-  for (int t = 0; t < T; ++t) {
-    const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
-    const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
-    const int S = tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H, 0, nullptr, nullptr, 0, nullptr,
-                        nullptr, true);
-    hipLaunchKernelGGL(k_tr_cell_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, S > 1 ? gc.split : s.G4, S,
-                       s.PRE + (size_t)t * B * 5 * H, 5 * H, cp, B, H, s.Hs + (size_t)t * B * H,
-                       s.Cs + (size_t)t * B * H, s.GA + (size_t)t * B * 4 * H);
+  if (gc.bf16) {
+    // one fused launch per step (k_tr_lstm_f), W_hh packed to bf16 fragments once
+    hipLaunchKernelGGL(k_pk_whh, dim3(nblk((int64_t)4 * H * H / 8)), dim3(256), 0, st, w->lstm_w_hh, H, 0, s.whf);
+    const unsigned grid = (unsigned)(((B + 15) / 16) * (H / 16));
+    for (int t = 0; t < T; ++t) {
+      const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
+      const float* pre = s.PRE + (size_t)t * B * 5 * H;
+      float *ho = s.Hs + (size_t)t * B * H, *co = s.Cs + (size_t)t * B * H, *ga = s.GA + (size_t)t * B * 4 * H;
+#define AA_LF(H_)                                                                                                  \
+  if (t == 0)                                                                                                      \
+    hipLaunchKernelGGL((k_tr_lstm_f<H_, true>), dim3(grid), dim3(256), 0, st, B, (const void*)s.h0, pre, 5 * H, cp, \
+                       s.whf, ho, co, ga, s.hb[0]);                                                              \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_tr_lstm_f<H_, false>), dim3(grid), dim3(256), 0, st, B, (const void*)s.hb[(t - 1) & 1],  \
+                       pre, 5 * H, cp, s.whf, ho, co, ga, s.hb[t & 1])
+      switch (H) {
+        case 256: AA_LF(256); break;
+        case 512: AA_LF(512); break;
+        case 768: AA_LF(768); break;
+        default: AA_LF(1024); break;
+      }
+#undef AA_LF
+    }
+  } else {
+    for (int t = 0; t < T; ++t) {
+      const float* hp = t ? s.Hs + (size_t)(t - 1) * B * H : s.h0;
+      const float* cp = t ? s.Cs + (size_t)(t - 1) * B * H : s.c0;
+      const int S = tgemm(gc, B, 4 * H, H, hp, H, 0, w->lstm_w_hh, H, 0, s.G4, 4 * H, 0, nullptr, nullptr, 0, nullptr,
+                          nullptr, true);
+      hipLaunchKernelGGL(k_tr_cell_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, S > 1 ? gc.split : s.G4, S,
+                         s.PRE + (size_t)t * B * 5 * H, 5 * H, cp, B, H, s.Hs + (size_t)t * B * H,
+                         s.Cs + (size_t)t * B * H, s.GA + (size_t)t * B * 4 * H);
+    }
   }
   // sentinel (adaptive_attention.py:79-83, h_{t-1} = [0, h_0 .. h_{T-2}], :116-120)
   hipLaunchKernelGGL(k_copy_cols, dim3(nblk((int64_t)R * H)), dim3(256), 0, st, s.PRE, (int64_t)5 * H, 4 * H, s.SG,
@@ -1389,16 +1584,44 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
   // LSTM backward through time (baseline_attention.py:167-178)
   AA_TRY(hipMemsetAsync(s.dh_rec, 0, (size_t)((char*)(s.dc_rec + (size_t)B * H) - (char*)s.dh_rec), st));  // adjacent
-  int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
-  for (int t = T - 1; t >= 0; --t) {
-    const size_t o = (size_t)t * B * H;
-    const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
-    hipLaunchKernelGGL(k_tr_cell_bwd_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o,
-                       S > 1 ? gc.split : s.dh_rec, S, s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H,
-                       s.DG + (size_t)t * B * 4 * H);
-    // dh_{t-1}; the one of step 0 (into h0) is reduced into dh_rec itself
-    S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H, 0, nullptr,
-              nullptr, 0, nullptr, nullptr, t > 0);
+  if (gc.bf16) {
+    // one fused launch per step (k_tr_lstm_b: dh_rec = DG_{t+1} W_hh, then the cell backward); the
+    // gradient into h0 (dh_rec of step 0) is one GEMM after the loop
+    hipLaunchKernelGGL(k_pk_whh, dim3(nblk((int64_t)4 * H * H / 8)), dim3(256), 0, st, w->lstm_w_hh, H, 1, s.whb);
+    const unsigned grid = (unsigned)(((B + 15) / 16) * (H / 16));
+    for (int t = T - 1; t >= 0; --t) {
+      const size_t o = (size_t)t * B * H;
+      const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
+      const float* ga = s.GA + (size_t)t * B * 4 * H;
+      float* dg = s.DG + (size_t)t * B * 4 * H;
+#define AA_LB(H_)                                                                                                   \
+  if (t == T - 1)                                                                                                   \
+    hipLaunchKernelGGL((k_tr_lstm_b<H_, true>), dim3(grid), dim3(256), 0, st, B, (const __bf16*)nullptr, s.whb,     \
+                       s.dH + o, s.dC + o, s.dc_rec, ga, s.Cs + o, cp, dg, s.dgb[t & 1]);                           \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k_tr_lstm_b<H_, false>), dim3(grid), dim3(256), 0, st, B, (const __bf16*)s.dgb[(t + 1) & 1], \
+                       s.whb, s.dH + o, s.dC + o, s.dc_rec, ga, s.Cs + o, cp, dg, s.dgb[t & 1])
+      switch (H) {
+        case 256: AA_LB(256); break;
+        case 512: AA_LB(512); break;
+        case 768: AA_LB(768); break;
+        default: AA_LB(1024); break;
+      }
+#undef AA_LB
+    }
+    tgemm(gc, B, H, 4 * H, s.DG, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);
+  } else {
+    int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
+    for (int t = T - 1; t >= 0; --t) {
+      const size_t o = (size_t)t * B * H;
+      const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
+      hipLaunchKernelGGL(k_tr_cell_bwd_sk, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dH + o, s.dC + o,
+                         S > 1 ? gc.split : s.dh_rec, S, s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H,
+                         s.DG + (size_t)t * B * 4 * H);
+      // dh_{t-1}; the one of step 0 (into h0) is reduced into dh_rec itself
+      S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H, 0, nullptr,
+                nullptr, 0, nullptr, nullptr, t > 0);
+    }
   }
   tgemm(gc, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
   tgemm(gc, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);

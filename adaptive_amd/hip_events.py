@@ -40,15 +40,36 @@ def hip() -> ctypes.CDLL:
     return _hip
 
 
-# hipEventDisableSystemFence | hipEventReleaseToDevice: timing-only events -- no system-scope fence
-# (cache writeback / invalidate) when the event is recorded, a device-scope release instead, so the
-# kernels between two events are timed without the fence's cost (hip_runtime_api.h)
-TIMING_FLAGS = 0x20000000 | 0x40000000
+# timing-only events: hipEventReleaseToDevice (a device-scope release when the event is recorded
+# instead of a system-scope one: no cache writeback / invalidate between the timed kernels), else
+# hipEventDisableSystemFence, else a default event -- the first flag set this HIP runtime accepts
+# (hip_runtime_api.h); ``timing_flags_used()`` names it
+TIMING_FLAG_CHOICES = (("hipEventReleaseToDevice", 0x40000000), ("hipEventDisableSystemFence", 0x20000000),
+                       ("hipEventDefault", 0x0))
+_timing_flags = None
+
+
+def _create_timing_event(ev) -> int:
+    global _timing_flags
+    h = hip()
+    if _timing_flags is not None:
+        return h.hipEventCreateWithFlags(ctypes.byref(ev), _timing_flags[1])
+    rc = -1
+    for name, flags in TIMING_FLAG_CHOICES:
+        rc = h.hipEventCreateWithFlags(ctypes.byref(ev), flags)
+        if rc == 0:
+            _timing_flags = (name, flags)
+            break
+    return rc
+
+
+def timing_flags_used() -> str:
+    return _timing_flags[0] if _timing_flags else "none yet"
 
 
 class EventArray:
     """n raw hipEvent_t handles as a C array (pass ``.ptr`` as an ``aa_event_t*``).  ``precise``:
-    timing-only events (TIMING_FLAGS), the default for per-kernel timing."""
+    timing-only events (``_create_timing_event``), the default for per-kernel timing."""
 
     def __init__(self, n: int, precise: bool = True):
         self.n = n
@@ -56,8 +77,7 @@ class EventArray:
         h = hip()
         for i in range(n):
             ev = c_void_p()
-            rc = (h.hipEventCreateWithFlags(ctypes.byref(ev), TIMING_FLAGS) if precise
-                  else h.hipEventCreate(ctypes.byref(ev)))
+            rc = _create_timing_event(ev) if precise else h.hipEventCreate(ctypes.byref(ev))
             if rc != 0:
                 raise RuntimeError(f"hipEventCreate failed: {rc}")
             self.arr[i] = ev.value

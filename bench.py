@@ -53,7 +53,7 @@ sys.path.insert(0, ROOT)
 from adaptive_amd import Config, Encoder2Decoder, synth  # noqa: E402
 from adaptive_amd import _lib  # noqa: E402
 from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
-from adaptive_amd.hip_events import EventArray  # noqa: E402
+from adaptive_amd.hip_events import EventArray, timing_flags_used  # noqa: E402
 from adaptive_amd.distributed import gather_rows  # noqa: E402
 from adaptive_amd.pipeline import DecodePipeline  # noqa: E402
 
@@ -529,8 +529,8 @@ def main():
         roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"],
-                    "duration_source": "timing-only HIP events (hipEventDisableSystemFence | hipEventReleaseToDevice) "
-                                       "on the launch stream around each launch, traced region"}
+                    "duration_source": f"HIP events ({timing_flags_used()}) on the launch stream around each "
+                                       f"launch, traced region"}
         if dominant == "k_atten":
             vb = v_restream_bytes_per_row() * B
             mall = read_probe(dev, vb)
