@@ -453,9 +453,13 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m0 = blockIdx.x * E4_ROWS;
   // staging: thread t < 392 -> row r = t % 98, channels 8 kg .. 8 kg + 7 of each 32-channel stage;
-  // threads 392..511 fill garbage rows 98..105 (never stored) from a valid address
+  // threads 392..511 fill garbage rows 98..105 (never stored) from a valid address.  (Each 8-lane
+  // group of the ds_write_b128 then hits 4 distinct 16-B slots: 2-way store conflicts.  Remapping the
+  // groups to 4 rows x 2 channel groups removes them but splits each wave's 256-B row-contiguous
+  // feature loads into 128-B pieces: measured 246 -> 256 us, not kept.)
   const int sr = t < 4 * E4_ROWS ? t % E4_ROWS : E4_ROWS + (t & 7);
   const int kg = t < 4 * E4_ROWS ? t / E4_ROWS : (t >> 3) & 3;
+  const bool stg = stager;
   int m = m0 + (t < 4 * E4_ROWS ? sr : 0);
   m = m < M ? m : M - 1;  // clamp, never zero (rows >= M are not stored)
   const int bi = m / P, pi = m - bi * P;
@@ -500,16 +504,16 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   };
 
   const int ns = KC;
-  if (stager) gload_a(0);
+  if (stg) gload_a(0);
 #pragma unroll
   for (int c = 0; c < NCB; ++c) gload_w(0, c);
-  if (stager) lstore_a(0);
-  if (stager) gload_a(ns > 1 ? 1 : 0);
+  if (stg) lstore_a(0);
+  if (stg) gload_a(ns > 1 ? 1 : 0);
   __syncthreads();
   for (int s = 0; s < ns; ++s) {
     const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
     // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
-    if (stager) {
+    if (stg) {
       lstore_a(buf ^ 1);
       gload_a(s2);
     }
@@ -591,189 +595,6 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
     }
     __syncthreads();
     constexpr int F4 = 16 * H / 4;  // float4s of the block
-#pragma unroll
-    for (int q = t; q < F4; q += NT) {
-      const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
-      if (tr < E4_ROWS && row < M)
-        *reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4) = *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// E1' (k_enc_v5, the default at H = 512 / 256): k_enc_v4's workgroup (two images, all H columns),
-// MFMA order and epilogue -- bit-identical V -- restructured around the LDS:
-//  * 64-channel stages (two 32-channel chunks) instead of 32: half the barriers (32 per workgroup),
-//    and a stage's loads get two chunks of MFMA work to land behind;
-//  * no fp32 stage copy for the avg-pool: every fp32 x is exactly h + m + l of its three bf16
-//    planes (RNE split: x - h has <= 16 significant bits, its remainder after m <= 8), and
-//    ((float)h + (float)m) + (float)l reproduces it exactly, so one wave per stage rebuilds each
-//    channel's 49 values from the A planes already in LDS and sums them in p order (k_avgpool's
-//    arithmetic, bit-identical a_g, written straight to memory: no a_g array in LDS either);
-//  * staging stores without bank conflicts: a ds_write_b128 is serviced in groups of 8 contiguous
-//    lanes on 32 banks, and 8 consecutive rows at the 96-B pitch (6 16-B slots) hit only 4 distinct
-//    slots; each group of 8 lanes now takes 4 rows x 2 channel groups: slots (6 j + k) mod 8, j < 4,
-//    k < 2, are all distinct.  The 96-B pitch stays (conflict-free ds_read_b128 fragment reads);
-//  * every wave stages (800 staging lanes: 25 four-row blocks x 2 chunks x 2 channel-group pairs).
-// LDS: [2 buffers][2 chunks][3 planes][112 rows][48] bf16, each chunk's planes 64 B apart from the
-// other's (the avg-pool's dword reads of the two chunks land on different banks) = 126 KB.
-// ---------------------------------------------------------------------------------------------
-constexpr int E5_PL = 7 * 16 * E4_LD;           // one plane of one chunk (bf16)
-constexpr int E5_CH = 3 * E5_PL + 32;           // one chunk: 3 planes + 64 B
-constexpr int E5_BUF = 2 * E5_CH;               // one 64-channel stage
-constexpr int E5_TASKS = 25 * 2 * 2 * 8;        // staging lanes (rows 98, 99 clamp to valid rows, never stored)
-template <int NCB, int NW>
-__global__ __launch_bounds__(64 * NW) void k_enc_v5(const float* __restrict__ feats, int B, int C,
-                                                const bf16x8* __restrict__ W4, const float* __restrict__ bias,
-                                                float* __restrict__ V, float* __restrict__ a_g) {
-  static_assert(NCB % 2 == 0, "columns are processed in pairs of 16-column blocks");
-  constexpr int H = 16 * NCB * NW, NPAIR = NCB / 2;
-  constexpr int NT = 64 * NW, ST = (E5_TASKS + NT - 1) / NT;  // staging tasks per thread
-  __shared__ __attribute__((aligned(16))) __bf16 As[2 * E5_BUF];
-  const int M = B * P, KC = C / 32, NS = C / 64;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = blockIdx.x * E4_ROWS;
-  // staging task q (lane group g8 = q >> 3, i = q & 7): rows 4 rb + (i & 3) of four-row block rb =
-  // g8 % 25, chunk hp >> 1 and channel group 2 (hp & 1) + (i >> 2) (8 channels) of it, hp = g8 / 25
-  const float* src[ST];
-  int so[ST];
-  bool act[ST];
-#pragma unroll
-  for (int j = 0; j < ST; ++j) {
-    const int q = t + j * NT;
-    act[j] = q < E5_TASKS;
-    const int g8 = act[j] ? q >> 3 : 0, i = q & 7;
-    const int rb = g8 % 25, hp = g8 / 25, ch = hp >> 1, kg = 2 * (hp & 1) + (i >> 2);
-    const int r = 4 * rb + (i & 3);
-    int m = m0 + (r < E4_ROWS ? r : E4_ROWS - 1);
-    m = m < M ? m : M - 1;  // clamp, never zero (rows >= M and r >= 98 are not stored)
-    const int bi = m / P, pi = m - bi * P;
-    src[j] = feats + (int64_t)bi * C * P + pi + (int64_t)(32 * ch + 8 * kg) * P;
-    so[j] = ch * E5_CH + r * E4_LD + 8 * kg;
-  }
-  const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);  // fragment reads: row 16 rb + (l & 15), k 8 (l >> 4)
-  const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;
-  float ra[ST][8];
-  bf16x8 wv[NCB][3];
-  floatx4 acc[E4_RB][NCB];
-#pragma unroll
-  for (int rb = 0; rb < E4_RB; ++rb)
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) acc[rb][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto gload_a = [&](int s) {
-#pragma unroll
-    for (int j = 0; j < ST; ++j)
-      if (act[j]) {
-        const float* sp = src[j] + (int64_t)(64 * s) * P;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ra[j][i] = AA_FEAT_LOAD(sp + i * P);
-      }
-  };
-  auto gload_w = [&](int kc, int c) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)kc * 3 + q) * 64];
-  };
-  auto lstore_a = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < ST; ++j)
-      if (act[j]) {
-        bf16x8 x[3];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __bf16 x0, x1, x2;
-          split3(ra[j][i], x0, x1, x2);
-          x[0][i] = x0; x[1][i] = x1; x[2][i] = x2;
-        }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&As[buf * E5_BUF + so[j] + q * E5_PL]) = x[q];
-      }
-  };
-  gload_a(0);
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) gload_w(0, c);
-  lstore_a(0);
-  gload_a(NS > 1 ? 1 : 0);
-  __syncthreads();
-  for (int s = 0; s < NS; ++s) {
-    const int buf = s & 1, s2 = s + 2 < NS ? s + 2 : NS - 1;
-    // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
-    lstore_a(buf ^ 1);
-    gload_a(s2);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kc = 2 * s + h, kn = kc + 1 < KC ? kc + 1 : KC - 1;
-      const __bf16* Ab = &As[buf * E5_BUF + h * E5_CH + fo];
-#pragma unroll
-      for (int cp = 0; cp < NPAIR; ++cp) {
-#pragma unroll
-        for (int rb = 0; rb < E4_RB; ++rb) {
-          bf16x8 fa[3];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(Ab + q * E5_PL + rb * 16 * E4_LD);
-          const int c0 = 2 * cp, c1 = c0 + 1;
-          floatx4 x = acc[rb][c0], y = acc[rb][c1];
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c0][0], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wv[c1][0], y, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][1], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][1], y, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][2], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][2], y, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c0][0], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wv[c1][0], y, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][1], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][1], y, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c0][0], x, 0, 0, 0);
-          y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wv[c1][0], y, 0, 0, 0);
-          acc[rb][c0] = x;
-          acc[rb][c1] = y;
-        }
-        gload_w(kn, 2 * cp);
-        gload_w(kn, 2 * cp + 1);
-        asm volatile("" ::: "memory");
-      }
-    }
-    // one wave per stage (rotating) rebuilds the stage's 2 images x 64 channels from the three planes
-    // and sums them in p order: lane -> image lane >> 5, channels 2 (lane & 31), + 1 (chunk (lane >> 4) & 1)
-    if (wave == (s % NW)) {
-      const int img = lane >> 5, cpair = lane & 31, ch = cpair >> 4, cl = 2 * (cpair & 15);
-      const __bf16* pb = &As[buf * E5_BUF + ch * E5_CH + (img * P) * E4_LD + cl];
-      float s0 = 0.f, s1 = 0.f;
-      for (int pp = 0; pp < P; ++pp) {
-        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD);
-        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD + E5_PL);
-        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(pb + pp * E4_LD + 2 * E5_PL);
-        s0 += (__uint_as_float(w0 << 16) + __uint_as_float(w1 << 16)) + __uint_as_float(w2 << 16);
-        s1 += (__uint_as_float(w0 & 0xFFFF0000u) + __uint_as_float(w1 & 0xFFFF0000u)) + __uint_as_float(w2 & 0xFFFF0000u);
-      }
-      const int b = 2 * blockIdx.x + img;
-      if (b < B) {
-        float* dst = a_g + (int64_t)b * C + 64 * s + 32 * ch + cl;
-        dst[0] = s0 / 49.0f;
-        dst[1] = s1 / 49.0f;
-      }
-    }
-    __syncthreads();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // epilogue (as k_enc_v4): each 16-row block through LDS, out as whole contiguous rows of V
-  float* Vs = reinterpret_cast<float*>(&As[0]);
-  constexpr int VSP = H + 4;
-  static_assert(16 * VSP * 4 <= sizeof(As), "V staging must fit in the A stages");
-  float bvs[NCB];
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) bvs[c] = bias[(wave * NCB + c) * 16 + (lane & 15)];
-#pragma unroll
-  for (int rb = 0; rb < E4_RB; ++rb) {
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      const int col = (wave * NCB + c) * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Vs[(4 * (lane >> 4) + i) * VSP + col] = reluf_(acc[rb][c][i] + bvs[c]);
-    }
-    __syncthreads();
-    constexpr int F4 = 16 * H / 4;
 #pragma unroll
     for (int q = t; q < F4; q += NT) {
       const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
@@ -2667,14 +2488,6 @@ static bool enc_v4(const Layout& L, int32_t flags) {
 static bool gemm3_ok(int32_t flags, int K) {
   return !(flags & AA_DECODE_FP32_ENCODER) && K % 256 == 0;
 }
-// k_enc_v5 (64-channel stages) unless AA_ENC_V4=1 (A/B of the two encoders; bit-identical outputs)
-static bool enc_v5() {
-  static const bool v = [] {
-    const char* e = getenv("AA_ENC_V4");
-    return !(e && atoi(e) == 1);
-  }();
-  return v;
-}
 // hsp0 != nullptr (greedy decode): h0 split into the 3-plane fragments k_lstm reads, on `s` after the
 // VWv GEMM, waiting for the heads only (the aux stream's x_g GEMM is still running: off the critical path)
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
@@ -2724,17 +2537,11 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     rec(ev, 1, s);
     rec(ev, 2, s);
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
-    if (enc_v5()) {
-      if (H == 512)
-        hipLaunchKernelGGL((k_enc_v5<2, 16>), dim3(nwg), dim3(1024), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-      else
-        hipLaunchKernelGGL((k_enc_v5<2, 8>), dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-    } else if (H == 512) {
+    if (H == 512)
       hipLaunchKernelGGL((k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg),
                          dim3(64 * AA_ENC4_NW), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-    } else {
+    else
       hipLaunchKernelGGL(k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-    }
     rec(ev, 3, s);
     if (sa != s) {  // aux waits for a_g
       hipEvent_t agr = nullptr;

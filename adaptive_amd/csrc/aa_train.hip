@@ -504,6 +504,44 @@ __global__ __launch_bounds__(256) void k_pk_featrows(const float* __restrict__ f
   }
 }
 
+// One pass over the NCHW feature map for a bf16 step: a workgroup per (image, 64 channels) reads its
+// 64 x 49 contiguous floats once and writes (1) the rows of the encoder GEMM's operand, as
+// k_pk_featrows; (2) the K-contiguous operand of the backward's dW_a = dV^T A, cols[c][b 49 + p] (as
+// k_pk_feats, zero past row B 49 up to Kp: the last image's workgroups); (3) a_g[b][c] = the 49 values
+// summed in p order / 49 -- k_avgpool's arithmetic, bit-identical.  Replaces k_avgpool +
+// k_pk_featrows + the backward's k_pk_feats (three reads of the map, one now).
+__global__ __launch_bounds__(256) void k_pk_feats3(const float* __restrict__ feats, int B, int C,
+                                                   __bf16* __restrict__ rows, __bf16* __restrict__ cols, int Kp,
+                                                   float* __restrict__ a_g) {
+  __shared__ float tile[64 * P];
+  const int b = blockIdx.y, c0 = blockIdx.x * 64, t = threadIdx.x;
+  const float* src = feats + ((int64_t)b * C + c0) * P;
+  for (int i = t; i < 64 * P; i += 256) tile[i] = src[i];  // [c][p]
+  __syncthreads();
+  for (int i = t; i < P * 8; i += 256) {  // row p, 8-channel piece j
+    const int p = i >> 3, j = i & 7;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)tile[(8 * j + e) * P + p];
+    *reinterpret_cast<bf16x8*>(rows + ((int64_t)b * P + p) * C + c0 + 8 * j) = v;
+  }
+  for (int i = t; i < 64 * P; i += 256) {
+    const int c = i / P, p = i - c * P;
+    cols[(int64_t)(c0 + c) * Kp + b * P + p] = (__bf16)tile[i];
+  }
+  if (b == B - 1)
+    for (int i = t; i < 64 * (Kp - B * P); i += 256) {
+      const int c = i / (Kp - B * P), r = B * P + i % (Kp - B * P);
+      cols[(int64_t)(c0 + c) * Kp + r] = (__bf16)0.f;
+    }
+  if (t < 64) {
+    const float* g = tile + t * P;
+    float sum = 0.f;
+    for (int p = 0; p < P; ++p) sum += g[p];
+    a_g[(int64_t)b * C + c0 + t] = sum / 49.0f;
+  }
+}
+
 // the NCHW feature map as the K-contiguous operand of dW_a = dV^T A: dst[c][b 49 + p] = feats[b][c][p],
 // zero for rows >= B 49 up to Kp; 8 consecutive rows per thread (one 16-B store)
 __global__ void k_pk_feats(const float* __restrict__ feats, int B, int C, __bf16* __restrict__ dst, int Kp) {
@@ -693,6 +731,106 @@ __global__ __launch_bounds__(256) void k_tr_atten(int B, int H, const float* __r
   }
 }
 
+// k_tr_atten's rows grouped by image: one workgroup per (image b, group of TS consecutive steps)
+// keeps V_b in registers (thread t owns columns t + 256 j, j < HPT: 49 HPT floats) and VWv_b in LDS,
+// and runs its rows one after another with the next row's small operands (PG, PS rows; S, h, the
+// row's columns) loaded ahead -- V_b and VWv_b are read once per group instead of once per row (2304
+// x 100 KB per training step at B = 128, T = 18), and every row's arithmetic is k_tr_atten's, in the
+// same order (scores by one wave per item, the two softmaxes by wave 0, the context as one fma chain
+// over k per column): bit-identical outputs.
+template <int HPT>
+__global__ __launch_bounds__(256) void k_tr_atten_img(int B, int T, int TS, const float* __restrict__ PG,
+                                                      const float* __restrict__ PS, const float* __restrict__ VWv,
+                                                      const float* __restrict__ Vf, const float* __restrict__ wh,
+                                                      const float* __restrict__ Hs, const float* __restrict__ S,
+                                                      float* __restrict__ alpha, float* __restrict__ beta,
+                                                      float* __restrict__ ctx, float* __restrict__ U) {
+  constexpr int H = 256 * HPT;
+  __shared__ float s_vwv[P * PP], zs[PP], al[PP], sh_b;
+  const int b = blockIdx.x, t0 = blockIdx.y * TS, t1 = t0 + TS < T ? t0 + TS : T;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t0 >= t1) return;
+  float v[P][HPT];
+  const float* vb = Vf + (int64_t)b * P * H;
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) v[k][j] = vb[(int64_t)k * H + t + 256 * j];
+  for (int e = t; e < P * PP; e += 256) s_vwv[e] = VWv[(int64_t)b * P * PP + e];
+  const float whl = lane < P ? wh[lane] : 0.f;
+  // row operands, loaded one row ahead
+  auto ld_small = [&](int r, float& pg, float& ps) {
+    pg = lane < P ? PG[(int64_t)r * PP + lane] : 0.f;
+    ps = lane < P ? PS[(int64_t)r * PP + lane] : 0.f;
+  };
+  auto ld_cols = [&](int r, float (&sv)[HPT], float (&hv)[HPT]) {
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) {
+      sv[j] = S[(int64_t)r * H + t + 256 * j];
+      hv[j] = Hs[(int64_t)r * H + t + 256 * j];
+    }
+  };
+  float pg, ps, sv[HPT], hv[HPT];
+  ld_small(t0 * B + b, pg, ps);
+  ld_cols(t0 * B + b, sv, hv);
+  __syncthreads();  // s_vwv
+  for (int st = t0; st < t1; ++st) {
+    const int r = st * B + b;
+    for (int k = w; k <= P; k += 4) {
+      float z = 0.f;
+      if (lane < P) {
+        const float x = (k < P ? s_vwv[k * PP + lane] : ps) + pg;
+        z = whl * tanhf(x);
+      }
+      z = wave_sum(z);
+      if (lane == 0) zs[k] = z;
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float z = lane < P ? zs[lane] : -INFINITY;
+      const float m = wave_max(z);
+      const float e = lane < P ? expf(z - m) : 0.f;
+      const float a = e / wave_sum(e);
+      if (lane < P) {
+        al[lane] = a;
+        alpha[(int64_t)r * PP + lane] = a;
+      }
+      const float zsn = zs[P];
+      const float m2 = fmaxf(m, zsn);
+      const float e2 = lane < P ? expf(z - m2) : 0.f;
+      const float es = expf(zsn - m2);
+      const float S2 = wave_sum(e2) + es;
+      if (lane == 0) {
+        sh_b = es / S2;
+        beta[r] = es / S2;
+      }
+    }
+    __syncthreads();
+    const float be = sh_b;
+    float svc[HPT], hvc[HPT];
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) {
+      svc[j] = sv[j];
+      hvc[j] = hv[j];
+    }
+    if (st + 1 < t1) {  // the next row's operands, in flight under this row's context
+      ld_small(r + B, pg, ps);
+      ld_cols(r + B, sv, hv);
+    }
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) {
+      const int d = t + 256 * j;
+      float c = 0.f;
+#pragma unroll
+      for (int k = 0; k < P; ++k) c = __builtin_fmaf(al[k], v[k][j], c);
+      ctx[(int64_t)r * H + d] = c;
+      const float chat = be * svc[j] + (1.f - be) * c;
+      U[(int64_t)r * H + d] = chat + hvc[j];
+    }
+    __syncthreads();  // al / sh_b / zs are rewritten by the next row
+  }
+}
+
 // packed row map: prow[p] = t B + b for the rows of pack_padded_sequence (lengths sorted desc)
 __global__ void k_tr_prow(const int* __restrict__ len, int B, int T, int* __restrict__ prow) {
   // one thread per (t, b); batch size of t = #{b : len[b] > t}; offset = sum of earlier sizes
@@ -738,14 +876,21 @@ __global__ __launch_bounds__(256) void k_tr_atb_row(int B, const int* __restrict
                                                     const float* __restrict__ VWv, const float* __restrict__ Vf,
                                                     const float* __restrict__ wh, float* __restrict__ dS,
                                                     float* __restrict__ dPG, float* __restrict__ dPS,
-                                                    float* __restrict__ dz_out, float* __restrict__ dwr) {
+                                                    float* __restrict__ dz_out, float* __restrict__ dwr,
+                                                    float* __restrict__ dH) {
   constexpr int H = 256 * HPT;
   __shared__ float s_al[PP], s_da[PP], s_dz[PP], s_red[4], s_dzs;
   __shared__ float s_dc[H];
   __shared__ float s_cv[P * P], s_tz[P * P];
   const int r = blockIdx.x, b = r % B, tt = r / B;
-  if (tt >= len[b]) return;  // uniform over the workgroup
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // dh = dU (u = c_hat + h; the recurrent GEMMs add into dH later): written here for every row, zero
+  // for the rows past a caption's length (their dU is zero: no loss gradient)
+  if (tt >= len[b]) {  // uniform over the workgroup
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) dH[(int64_t)r * H + t + 256 * i] = 0.f;
+    return;
+  }
   const float* vb = Vf + (int64_t)b * P * H;
   const float whj = t < P ? wh[t] : 0.f;
   const float be = beta[r];
@@ -754,6 +899,7 @@ __global__ __launch_bounds__(256) void k_tr_atb_row(int B, const int* __restrict
   for (int i = 0; i < HPT; ++i) {
     const int d = t + 256 * i;
     const float du = dU[(int64_t)r * H + d];
+    dH[(int64_t)r * H + d] = du;
     part += du * (S[(int64_t)r * H + d] - ctx[(int64_t)r * H + d]);
     dS[(int64_t)r * H + d] = be * du;
     s_dc[d] = (1.f - be) * du;
@@ -901,6 +1047,25 @@ __global__ void k_pad_rows(const float* __restrict__ src, int rows, int cols, in
   const float v = c < cols ? src[(int64_t)r * cols + c] : 0.f;
   if (dst) dst[i] = v;
   if (dstb) dstb[i] = (__bf16)v;
+}
+
+// bf16 steps: dscores [rows][cols] -> bf16 [rows][pitch] (zero columns past cols), with the column
+// sums of the bias gradient db_m taken on the way: thread = column n, grid.y = the 64 row chunks of
+// k_colsum, each chunk summed in row order into part[chunk][n] -- k_colsum's arithmetic on the same
+// values (k_colsum_fin then adds the chunks in order), so db_m is bit-identical and dscores is read
+// once instead of twice
+__global__ void k_pad_rows_colsum(const float* __restrict__ src, int rows, int cols, int pitch,
+                                  __bf16* __restrict__ dstb, float* __restrict__ part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, ch = blockIdx.y;
+  if (n >= pitch) return;
+  const int per = (rows + CS_CH - 1) / CS_CH, m0 = ch * per, m1 = m0 + per < rows ? m0 + per : rows;
+  float s = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    const float v = n < cols ? src[(int64_t)m * cols + n] : 0.f;
+    dstb[(int64_t)m * pitch + n] = (__bf16)v;
+    s += v;
+  }
+  if (n < cols) part[(int64_t)ch * cols + n] = s;
 }
 
 // gather rows: dst[i] = src[rows[i]]
@@ -1235,7 +1400,7 @@ struct TrainWS {
   float *dz, *dwr;  // per-row dz and w_h-gradient terms of k_tr_atb_row, summed per image by k_tr_atb_img
   // bf16 operands of the large GEMMs (AA_TRAIN_BF16, k_bgemm): U_p, W_m, dS (rows), W_m^T, dS^T, U_p^T,
   // dV^T, the feature map as [C][B 49]
-  __bf16 *ub, *wmb, *dspb, *wmT, *dspT, *upT, *dvT, *ftT;
+  __bf16 *ub, *wmb, *dspb, *wmT, *dspT, *upT, *dvT, *ftT, *ftC;
   // fused recurrent steps (bf16): W_hh as forward / backward B-fragments, h_t and DG_t ping-pong bf16 copies
   bf16x8 *whf, *whb;
   __bf16 *hb[2], *dgb[2];
@@ -1315,6 +1480,7 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
     w.upT = c.take<__bf16>(H * Kr);
     w.dvT = c.take<__bf16>(H * Kb);
     w.ftT = c.take<__bf16>(Cc * Kb);
+    w.ftC = c.take<__bf16>(Cc * Kb);  // [C][Kb]: the backward's dW_a operand, written by the forward's k_pk_feats3
     w.whf = c.take<bf16x8>(4 * H * H / 8);
     w.whb = c.take<bf16x8>(4 * H * H / 8);
     for (int i = 0; i < 2; ++i) {
@@ -1399,8 +1565,24 @@ static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const Train
   // attention projections and the attention itself (adaptive_attention.py:26-58)
   tgemm(gc, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
   tgemm(gc, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
-  hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs, s.S,
-                     s.alpha, s.beta, s.ctx, s.U);
+  {
+    // rows grouped by image (V_b read once per group): groups of TS steps so that the grid covers
+    // the chip (>= 256 workgroups when B is small)
+    int G = B > 0 ? (256 + B - 1) / B : 1;
+    G = G < T ? G : T;
+    const int TS = (T + G - 1) / G;
+    G = (T + TS - 1) / TS;
+#define AA_TRA(HPT_)                                                                                              \
+  hipLaunchKernelGGL(k_tr_atten_img<HPT_>, dim3(B, G), dim3(256), 0, st, B, T, TS, s.PG, s.PS, s.VWv, s.V,        \
+                     w->att_affine_h_w, s.Hs, s.S, s.alpha, s.beta, s.ctx, s.U)
+    switch (H) {
+      case 256: AA_TRA(1); break;
+      case 512: AA_TRA(2); break;
+      case 768: AA_TRA(3); break;
+      default: AA_TRA(4); break;
+    }
+#undef AA_TRA
+  }
 }
 
 int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
@@ -1419,14 +1601,14 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   hipStream_t st = (hipStream_t)stream;
   const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
   // encoder tail (baseline_attention.py:46-60), reference weight layouts
-  hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
   if (gc.bf16 && H % 64 == 0 && C % 64 == 0) {
-    // bf16 step: V = relu(A W_a^T + b) on k_bgemm (the feature map and W_a packed to bf16 in buffers the
-    // backward pass reuses for its own operands)
-    hipLaunchKernelGGL(k_pk_featrows, dim3(C / 64, B), dim3(256), 0, st, feats, C, s.ftT);
+    // bf16 step: V = relu(A W_a^T + b) on k_bgemm; one pass over the feature map packs both bf16
+    // operand layouts (this GEMM's rows, the backward's dW_a columns) and computes a_g
+    hipLaunchKernelGGL(k_pk_feats3, dim3(C / 64, B), dim3(256), 0, st, feats, B, C, s.ftT, s.ftC, rup64(B * P), s.a_g);
     pk_rows(st, w->enc_affine_a_w, C, nullptr, H, C, s.wmT, C);
     bgemm(gc, B * P, H, C, s.ftT, C, s.wmT, C, s.V, H, w->enc_affine_a_b, nullptr, 0, 1);
   } else {
+    hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
     hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, st, feats, B, C, H, w->enc_affine_a_w,
                        w->enc_affine_a_b, s.V);
@@ -1533,8 +1715,12 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   const bool bg = gc.bf16 && H % 64 == 0;  // the large GEMMs on k_bgemm
   // bf16 steps need dS only as bf16 (the GEMMs) and fp32 for db_m, which colsum reads from dscores
   // itself (same sums, same order): no fp32 re-pitched copy
-  hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp,
-                     bg ? nullptr : s.dsp, bg ? s.dspb : nullptr);
+  if (bg)  // dS to bf16 for the GEMMs, db_m's column partials on the way (finished below)
+    hipLaunchKernelGGL(k_pad_rows_colsum, dim3((Vp + 255) / 256, CS_CH), dim3(256), 0, st, dscores, N, V, Vp, s.dspb,
+                       s.csum);
+  else
+    hipLaunchKernelGGL(k_pad_rows, dim3(nblk((int64_t)N * Vp)), dim3(256), 0, st, dscores, N, V, Vp, s.dsp,
+                       (__bf16*)nullptr);
   // dU, dS, dPG, dPS are carved back to back: one clear for the four (nothing below touches dS / dPG
   // / dPS before the attention backward accumulates into them)
   AA_TRY(hipMemsetAsync(s.dU, 0, (size_t)((char*)(s.dPS + (size_t)R * PP) - (char*)s.dU), st));
@@ -1550,14 +1736,14 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
     tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
   }
-  if (bg) colsum(st, dscores, N, V, (int64_t)V, s.csum, GRAD(mlp_b));
+  if (bg) hipLaunchKernelGGL(k_colsum_fin, dim3((V + 255) / 256), dim3(256), 0, st, s.csum, V, GRAD(mlp_b));
   else colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
   // Atten backward (adaptive_attention.py:26-58)
   int G, TS;
   atb_groups(B, T, &G, &TS);
 #define AA_ATB(HPT_)                                                                                          \
   hipLaunchKernelGGL(k_tr_atb_row<HPT_>, dim3(R), dim3(256), 0, st, B, lengths, s.dU, s.alpha, s.beta, s.ctx, s.S, \
-                     s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, s.dz, s.dwr);                 \
+                     s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.dS, s.dPG, s.dPS, s.dz, s.dwr, s.dH);          \
   hipLaunchKernelGGL(k_tr_atb_img<HPT_>, dim3(B, HPT_ + 1), dim3(256), 0, st, B, TS, G, lengths, s.dU, s.alpha, s.beta, s.PG, \
                      s.VWv, w->att_affine_h_w, s.dz, s.dwr, s.dV, s.dVWv, s.dwh)
   switch (H / 256) {
@@ -1567,7 +1753,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     default: AA_ATB(4); break;
   }
 #undef AA_ATB
-  AA_TRY(hipMemcpyAsync(s.dH, s.dU, sizeof(float) * RH, hipMemcpyDeviceToDevice, st));  // u = c_hat + h
+  // dH = dU (u = c_hat + h) was written by k_tr_atb_row
   tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
   tgemm(gc, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
   tgemm(gc, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
@@ -1650,8 +1836,8 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   if (gc.bf16 && H % 64 == 0) {  // dW_a = dV^T A
     const int Kb = rup64(B * P);
     pk_trans(st, s.dV, H, B * P, H, s.dvT, Kb);
-    hipLaunchKernelGGL(k_pk_feats, dim3(nblk((int64_t)C * (Kb / 8))), dim3(256), 0, st, feats, B, C, s.ftT, Kb);
-    bgemm(gc, H, C, Kb, s.dvT, Kb, s.ftT, Kb, GRAD(enc_affine_a_w), C);
+    // the feature map's [C][Kb] bf16 operand was packed by the forward (k_pk_feats3, same workspace)
+    bgemm(gc, H, C, Kb, s.dvT, Kb, s.ftC, Kb, GRAD(enc_affine_a_w), C);
   } else {
     tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);              // dW_a = dV^T A
   }

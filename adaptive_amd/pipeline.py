@@ -51,25 +51,35 @@ class DecodePipeline:
     serialise.  (Slots replaying captured decode plans measured slower, DESIGN.md §4, and were
     removed.)
 
-    With ``raw_streams=True`` (default) the slots use the first ``depth`` of the process-wide list of
-    fresh HIP streams (``hip_events.raw_streams``): two pipelines alive on one device share those
-    streams and therefore serialise against each other (results stay correct; only their overlap is
-    lost)."""
+    With ``raw_streams=True`` (default) the first slot runs on the model's decode side stream (the
+    "decode-aux" role stream, idle while the pipeline runs: slots launch without a side stream) and the
+    others on the first ``depth - 1`` of the process-wide list of fresh HIP streams
+    (``hip_events.raw_streams``).  HIP hands a process's streams out round-robin over
+    GPU_MAX_HW_QUEUES (4) hardware queues, and the caller's stream and the decode side stream already
+    hold two: reusing the side stream keeps three slots on three distinct queues besides the caller's
+    (measured, depth 3, one box: 549 K captions/s against 444 K with three fresh streams, one of which
+    shared a queue).  Two pipelines alive on one device share those streams and therefore serialise
+    against each other (results stay correct; only their overlap is lost)."""
 
-    def __init__(self, model, max_len: int = 20, depth: int = 2, raw_streams: bool = True):
+    def __init__(self, model, max_len: int = 20, depth: int = 2, raw_streams: bool = True, streams=None):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.model, self.T, self.depth = model, int(max_len), int(depth)
         self.raw_streams = bool(raw_streams)
+        if streams is not None and len(streams) != self.depth:
+            raise ValueError("streams: one per batch in flight")
+        self._streams = streams
         self._slots = None
         self._pending = collections.deque()
         self._n = 0
 
     def _slot(self, dev) -> _Slot:
         if self._slots is None:
-            if self.raw_streams:  # fresh HIP streams: the slots land on distinct hardware queues
+            if self._streams is not None:
+                streams = list(self._streams)
+            elif self.raw_streams:  # the decode side stream + fresh HIP streams: distinct hardware queues
                 from .hip_events import raw_streams
-                streams = raw_streams(dev, self.depth)
+                streams = [self.model._aux_stream(dev)] + raw_streams(dev, self.depth - 1)
             else:
                 streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
             self._slots = [_Slot(dev, st) for st in streams]

@@ -29,9 +29,17 @@ for s in $steps; do
            python3 -c "import json;a=json.load(open('$out/train_bench.json'));print('train', round(a['value'],1), 'steps/s')" ;;
     trainprof) step trainprof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_train -o run --output-format csv -- python3 bench_train.py --no-cpu-baseline --steps 10 > $out/prof_train.log 2>&1
            f=$(find $out/prof_train -name '*kernel_stats.csv' | head -1); head -12 "$f" | cut -c1-140 ;;
-    abenc) for r in 1 2; do for v in 1 0; do
-             AA_ENC_V4=$v step abenc$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval-loop --pipeline-depth 1 --steps 20 > $out/ab_enc$v.$r.json 2>> $out/ab.err
-             python3 -c "import json;d=json.load(open('$out/ab_enc$v.$r.json'));k=d['kernels'];print('AA_ENC_V4=$v', round(d['value']), 'enc', round(k['k_enc_v4']['avg_ms']*1e3,1), 'us')"
+    ab) # A/B of an environment switch: AB_VAR=name (values 0 / 1), two interleaved rounds of short bench runs
+           for r in 1 2; do for v in 0 1; do
+             env ${AB_VAR:-AA_ENC_REMAP}=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval-loop --steps 20 > $out/ab$v.$r.json 2>> $out/ab.err; rc=$?
+             echo "[ab $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
+             python3 -c "import json;d=json.load(open('$out/ab$v.$r.json'));k=d['kernels'];print('${AB_VAR:-AA_ENC_REMAP}=$v', round(d['value']), 'pipe', round(d['pipelined']['value']), {n: round(e['avg_ms']*1e3,2) for n,e in k.items()})"
+           done; done ;;
+    pipe) # pipelined-rate probe: depth 2/3/4 x slot streams raw/aux
+           for ps in x; do for d in 2 3 4; do
+             timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval-loop --no-trace --steps 20 --pipeline-depth $d > $out/pipe_${ps}_$d.json 2>> $out/pipe.err; rc=$?
+             echo "[pipe $ps $d] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
+             python3 -c "import json;d=json.load(open('$out/pipe_${ps}_$d.json'));print('streams $ps depth $d seq', round(d['value']), 'pipe', round(d['pipelined']['value']))"
            done; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
