@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 # AA_LIB_PATH: load another build of the same library (A/B timing of two builds in one GPU session)
 LIB_PATH = os.environ.get("AA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                          "libadaptive_amd.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_ONE_STREAM = 512
@@ -108,6 +108,12 @@ SIGNATURES = {
     "aa_train_backward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p, c_int32,
                                   c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_void_p, c_size_t,
                                   c_int32, c_void_p]),
+    "aa_train_forward_aux": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p,
+                                     c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_size_t, c_int32, c_void_p,
+                                     c_void_p]),
+    "aa_train_backward_aux": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_int32, c_int32, c_void_p,
+                                      c_int32, c_void_p, c_void_p, c_int32, POINTER(RefWeights), c_void_p, c_void_p,
+                                      c_size_t, c_int32, c_void_p, c_void_p]),
     "aa_decoder_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
     "aa_decoder_forward": (c_int, [POINTER(RefWeights), POINTER(Dims), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                    c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

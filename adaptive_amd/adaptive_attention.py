@@ -522,6 +522,15 @@ class Encoder2Decoder(nn.Module):
         from .hip_events import role_stream
         return role_stream(dev, "decode-aux")
 
+    def _train_aux(self, dev):
+        """The second stream of aa_train_forward_aux / aa_train_backward_aux (the weight gradients and
+        the encoder's V GEMM beside the LSTM recurrence; bit-identical to one stream): the process's
+        "train-aux" role stream, or None (one stream) when ``train_aux_stream`` is False."""
+        if not getattr(self, "train_aux_stream", True):
+            return None
+        from .hip_events import role_stream
+        return role_stream(dev, "train-aux").cuda_stream
+
     def _train_flags(self) -> int:
         return _lib.TRAIN_BF16 if getattr(self, "train_bf16", False) else 0
 
@@ -708,9 +717,9 @@ class _TeacherForced(torch.autograd.Function):
         scores = torch.empty(N, owner.dims.vocab, device=images.device)
         w = _lib.RefWeights(*[p.data_ptr() for p in params])
         with torch.cuda.device(images.device):
-            rc = lib.aa_train_forward(w, d, images.data_ptr(), B, T, caps.data_ptr(), caps.stride(0),
-                                      len_dev.data_ptr(), scores.data_ptr(), N, ws.data_ptr(), nbytes,
-                                      owner._train_flags(), _lib.stream_handle())
+            rc = lib.aa_train_forward_aux(w, d, images.data_ptr(), B, T, caps.data_ptr(), caps.stride(0),
+                                          len_dev.data_ptr(), scores.data_ptr(), N, ws.data_ptr(), nbytes,
+                                          owner._train_flags(), _lib.stream_handle(), owner._train_aux(images.device))
         _lib.check(rc, "train_forward")
         ctx.owner, ctx.ws, ctx.N, ctx.T, ctx.flags = owner, ws, N, T, owner._train_flags()
         ctx.save_for_backward(images, caps, len_dev, *params)
@@ -728,9 +737,10 @@ class _TeacherForced(torch.autograd.Function):
         w = _lib.RefWeights(*[p.data_ptr() for p in params])
         g = _lib.RefWeights(*[t.data_ptr() for t in grads])
         with torch.cuda.device(images.device):
-            rc = lib.aa_train_backward(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(), caps.stride(0),
-                                       len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g, _lib.ptr(dfeats),
-                                       ctx.ws.data_ptr(), ctx.ws.numel(), ctx.flags, _lib.stream_handle())
+            rc = lib.aa_train_backward_aux(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(),
+                                           caps.stride(0), len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g,
+                                           _lib.ptr(dfeats), ctx.ws.data_ptr(), ctx.ws.numel(), ctx.flags,
+                                           _lib.stream_handle(), owner._train_aux(images.device))
         _lib.check(rc, "train_backward")
         ctx.ws = None
         return (None, dfeats, None, None, None, None, *grads)

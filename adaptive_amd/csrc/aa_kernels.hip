@@ -26,6 +26,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
+#include <vector>
 
 #include "aa_common.hpp"
 

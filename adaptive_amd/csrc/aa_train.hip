@@ -47,6 +47,7 @@ struct TG {
   int splits;   // split-K: > 1 -> raw partial tiles to part[split][M][N], reduced by k_tgemm_reduce
   int kper;     // K per split (multiple of the K step)
   float* part;
+  int* cnt;     // split-K with cnt != nullptr: the tile's last-arriving split combines in-launch (splitk_last)
 };
 
 // K step of the training GEMM: 64 with bf16 operands (two 32-wide halves per thread, so a
@@ -59,6 +60,98 @@ struct TStep {
   static constexpr int KS = BF ? 64 : 32, HH = KS / 32, LDK = KS + 4, LDB = KS + 8;
   static constexpr int TILE_F = BF ? 64 * LDB / 2 : 64 * LDK;  // one operand tile, in floats
 };
+
+// value i of a split GEMM: its S partials summed in split order from 0 (+ 0, as the reduce adds absent
+// biases), or src itself when it was not split.  Up to SK_MAX partials are loaded together before the
+// ordered sum (a loop over a runtime count waits for each load in turn).
+constexpr int SK_MAX = 16;
+__device__ __forceinline__ float sk_sum(const float* __restrict__ src, int S, int64_t MN, int64_t i) {
+  if (S == 1) return src[i];
+  float x[SK_MAX];
+#pragma unroll
+  for (int sp = 0; sp < SK_MAX; ++sp) x[sp] = sp < S ? src[sp * MN + i] : 0.f;
+  float v = 0.f;
+#pragma unroll
+  for (int sp = 0; sp < SK_MAX; ++sp)
+    if (sp < S) v += x[sp];
+  for (int sp = SK_MAX; sp < S; ++sp) v += src[sp * MN + i];
+  return v + 0.f;
+}
+
+// In-launch split-K combine (k_tgemm, k_bgemm): every split has stored its partial tile; the workgroup
+// that arrives last at the tile's device-scope counter sums the S partials of the tile in split order
+// and applies the epilogue -- exactly k_tgemm_reduce's arithmetic (sk_sum, then bias + bias2, act, row
+// map, accumulate), so the result is bit-identical, one launch (and its boundary) fewer per split
+// GEMM.  Hand-off (the guide's counter recipe in its write-through form): the partials were stored
+// sc1 (store_part: write-through, no release fence -- a per-thread __threadfence() measured 163
+// steps/s against 598, a lane-0 agent release 242: both write the XCD's L2 back), every wave drains
+// them, the workgroup meets at a barrier and lane 0 takes a ticket; the ticket S - 1 is the last
+// arriver, whose lane 0 acquires at agent scope before the workgroup reads the other splits' partials.  The
+// counters start at zero (cleared at the start of each training call) and the last arriver re-zeroes
+// its own.  `flag`: one int of the kernel's own LDS (its staging array, free after the main loop: no
+// second __shared__ object in the kernel).
+// TM x TN tile, 256 threads: thread -> column n0 + (t % TN), rows m0 + t / TN + (256 / TN) q.
+__device__ __forceinline__ void store_part(float* p, float v, bool sc1) {
+  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <int TM, int TN>
+__device__ __forceinline__ void splitk_last(int* flag, int* cnt, int tile, int S, const float* part, int M, int N, int m0, int n0,
+                            float* C, int64_t ldc, const int* crow, const float* bias, const float* bias2, int act,
+                            int accumulate) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    typedef __attribute__((address_space(1))) int gint;  // a global (not flat) agent-scope access
+    gint* c = (gint*)(cnt + tile);
+    const int last = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  constexpr int RS = 256 / TN, NQ = TM / RS, QC = NQ < 4 ? NQ : 4;  // rows in chunks of QC (registers)
+  const int n = n0 + (int)(threadIdx.x % TN), r0 = m0 + (int)(threadIdx.x / TN);
+  if (n >= N) return;
+  const int64_t MN = (int64_t)M * N;
+  const float bv = (bias ? bias[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
+  for (int q0 = 0; q0 < NQ; q0 += QC) {
+    float v[QC];
+#pragma unroll
+    for (int q = 0; q < QC; ++q) v[q] = 0.f;
+    // splits in order; the QC rows of up to 4 splits loaded together
+    for (int sp0 = 0; sp0 < S; sp0 += 4) {
+      float x[4][QC];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < QC; ++q) {
+          const int m = r0 + RS * (q0 + q);
+          x[j][q] = (sp0 + j < S && m < M) ? part[(int64_t)(sp0 + j) * MN + (int64_t)m * N + n] : 0.f;
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (sp0 + j < S)
+#pragma unroll
+          for (int q = 0; q < QC; ++q) v[q] += x[j][q];
+    }
+#pragma unroll
+    for (int q = 0; q < QC; ++q) {
+      const int m = r0 + RS * (q0 + q);
+      if (m >= M) continue;
+      float y = v[q] + 0.f;
+      y += bv;
+      if (act == 1) y = reluf_(y);
+      else if (act == 2) y = tanhf(y);
+      float* dst = C + (int64_t)(crow ? crow[m] : m) * ldc + n;
+      *dst = accumulate ? *dst + y : y;
+    }
+  }
+}
 
 // BF: operands rounded to bf16 (RNE) as they are staged in LDS, products on
 // v_mfma_f32_32x32x16_bf16 with fp32 accumulation (BASELINE config 5: bf16 compute, fp32 master
@@ -220,16 +313,20 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
     __syncthreads();
   }
   const int col = n0 + wnv * 32 + li;
-  if (col >= g.N) return;
   if (g.splits > 1) {
     float* pt = g.part + (int64_t)split * g.M * g.N;
+    if (col < g.N)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wmv * 32 + acc_row(r, lane);
-      if (m < g.M) pt[(int64_t)m * g.N + col] = acc[r];
-    }
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wmv * 32 + acc_row(r, lane);
+        if (m < g.M) store_part(pt + (int64_t)m * g.N + col, acc[r], g.cnt != nullptr);
+      }
+    if (g.cnt)
+      splitk_last<64, 64>(reinterpret_cast<int*>(&lds[0][0][0]), g.cnt, tile, g.splits, g.part, g.M, g.N, m0, n0, g.C, g.ldc, g.crow, g.bias, g.bias2, g.act,
+                          g.accumulate);
     return;
   }
+  if (col >= g.N) return;
   const float bv = (g.bias ? g.bias[col] : 0.f) + (g.bias2 ? g.bias2[col] : 0.f);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -241,23 +338,6 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
     float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
     *dst = g.accumulate ? *dst + v : v;
   }
-}
-
-// value i of a split GEMM: its S partials summed in split order from 0 (+ 0, as the reduce adds absent
-// biases), or src itself when it was not split.  Up to SK_MAX partials are loaded together before the
-// ordered sum (a loop over a runtime count waits for each load in turn).
-constexpr int SK_MAX = 16;
-__device__ __forceinline__ float sk_sum(const float* __restrict__ src, int S, int64_t MN, int64_t i) {
-  if (S == 1) return src[i];
-  float x[SK_MAX];
-#pragma unroll
-  for (int sp = 0; sp < SK_MAX; ++sp) x[sp] = sp < S ? src[sp * MN + i] : 0.f;
-  float v = 0.f;
-#pragma unroll
-  for (int sp = 0; sp < SK_MAX; ++sp)
-    if (sp < S) v += x[sp];
-  for (int sp = SK_MAX; sp < S; ++sp) v += src[sp * MN + i];
-  return v + 0.f;
 }
 
 // split-K epilogue: partials summed in split order, then bias / act / row map / accumulate
@@ -276,6 +356,16 @@ __global__ void k_tgemm_reduce(TG g) {
 // k_tgemm's split-K bound (floats of partials): its split counts, and so its fp32 sums, as before
 // the scratch grew for k_bgemm
 constexpr size_t TG_SPLIT_CAP = (size_t)4 << 20;
+constexpr int TR_CNT = 4096;  // split-K arrival counters (tiles) in a training workspace
+// the in-launch split-K combine (splitk_last) unless AA_SPLITK_REDUCE=1 (the separate k_tgemm_reduce
+// launch: bitwise A/B of the two forms)
+static int* splitk_counters(int* cnt) {
+  static const bool sep = [] {
+    const char* e = getenv("AA_SPLITK_REDUCE");
+    return e && atoi(e) == 1;
+  }();
+  return sep ? nullptr : cnt;
+}
 
 // launch context of a training call: stream + split-K scratch carved from its workspace
 struct GemmCtx {
@@ -283,6 +373,7 @@ struct GemmCtx {
   float* split;
   size_t cap;  // floats
   bool bf16;   // AA_TRAIN_BF16: bf16 operands, fp32 accumulation
+  int* cnt;    // split-K arrival counters (zero between launches): in-launch combine; nullptr = k_tgemm_reduce
 };
 
 // C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites.  GEMMs with
@@ -316,13 +407,15 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
     kper = ((K + splits - 1) / splits + ks - 1) / ks * ks;
     splits = (K + kper - 1) / kper;
   }
+  // split-K partials combined in-launch by each tile's last split (splitk_last) unless the consumer sums
+  // them itself (defer)
   TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, splits, kper,
-       splits > 1 ? gc.split : nullptr};
+       splits > 1 ? gc.split : nullptr, splits > 1 && !defer && tiles <= TR_CNT ? gc.cnt : nullptr};
   if (gc.bf16)
     hipLaunchKernelGGL(k_tgemm<true>, dim3(tiles * splits), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(k_tgemm<false>, dim3(tiles * splits), dim3(256), 0, s, g);
-  if (splits > 1 && !defer)
+  if (splits > 1 && !defer && !g.cnt)
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
   return splits;
 }
@@ -353,6 +446,7 @@ struct BG {
   int accumulate, splits, kper;
   float* part;
   int act;  // 0 none, 1 relu (after the bias)
+  int* cnt;  // split-K arrival counters: in-launch combine (splitk_last); nullptr = k_tgemm_reduce
 };
 __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BG_T * BG_LD];
@@ -435,7 +529,7 @@ __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
         const int m = m0 + wm * 64 + x * 32 + acc_row(r, lane);
         if (m >= g.M) continue;
         if (g.splits > 1) {
-          g.part[(int64_t)split * g.M * g.N + (int64_t)m * g.N + col] = acc[x][y][r];
+          store_part(g.part + (int64_t)split * g.M * g.N + (int64_t)m * g.N + col, acc[x][y][r], g.cnt != nullptr);
         } else {
           float v = acc[x][y][r] + bv;
           if (g.act == 1) v = reluf_(v);
@@ -444,6 +538,9 @@ __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
         }
       }
   }
+  if (g.splits > 1 && g.cnt)
+    splitk_last<BG_T, BG_T>(reinterpret_cast<int*>(&lds[0][0][0]), g.cnt, tile, g.splits, g.part, g.M, g.N, m0, n0, g.C, g.ldc, g.crow, g.bias, nullptr,
+                            g.act, g.accumulate);
 }
 
 // dst[r][k] = bf16(src[map ? map[r] : r][k]) for k < cols, 0 up to Kp (a multiple of 8): 8 per thread,
@@ -512,9 +609,11 @@ __global__ __launch_bounds__(256) void k_pk_featrows(const float* __restrict__ f
 // k_pk_featrows + the backward's k_pk_feats (three reads of the map, one now).
 __global__ __launch_bounds__(256) void k_pk_feats3(const float* __restrict__ feats, int B, int C,
                                                    __bf16* __restrict__ rows, __bf16* __restrict__ cols, int Kp,
-                                                   float* __restrict__ a_g) {
+                                                   float* __restrict__ a_g, int* __restrict__ clr, int nclr) {
   __shared__ float tile[64 * P];
   const int b = blockIdx.y, c0 = blockIdx.x * 64, t = threadIdx.x;
+  if (blockIdx.x == 0 && blockIdx.y == 0)  // (the training call's split-K arrival counters)
+    for (int i = t; i < nclr; i += 256) clr[i] = 0;
   const float* src = feats + ((int64_t)b * C + c0) * P;
   for (int i = t; i < 64 * P; i += 256) tile[i] = src[i];  // [c][p]
   __syncthreads();
@@ -577,9 +676,10 @@ static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64
   if (splits < 1) splits = 1;
   const int kper = (ksteps + splits - 1) / splits * BG_KS;
   splits = (K + kper - 1) / kper;
-  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr, act};
+  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr, act,
+             splits > 1 && tiles <= TR_CNT ? gc.cnt : nullptr};
   hipLaunchKernelGGL(k_bgemm, dim3(tiles * splits), dim3(256), 0, gc.s, g);
-  if (splits > 1) {
+  if (splits > 1 && !g.cnt) {
     TG r{};
     r.M = M; r.N = N; r.K = K; r.C = C; r.ldc = ldc; r.crow = crow; r.bias = bias; r.accumulate = accumulate;
     r.splits = splits; r.kper = kper; r.part = gc.split; r.act = act;
@@ -622,6 +722,59 @@ static void colsum(hipStream_t st, const float* X, int M, int N, int64_t ldx, fl
   hipLaunchKernelGGL(k_colsum, dim3((N + 255) / 256, CS_CH), dim3(256), 0, st, X, M, N, ldx, scratch);
   hipLaunchKernelGGL(k_colsum_fin, dim3((N + 255) / 256), dim3(256), 0, st, scratch, N, out);
 }
+
+// Two streams of one training call: `main` (the caller's) carries the chain the result depends on
+// step by step (encoder head -> LSTM -> attention -> vocab; its backward in reverse), `aux` the
+// work off that chain (the encoder's V GEMM beside the LSTM forward, the weight gradients beside
+// the LSTM backward).  Each side has its own split-K scratch, arrival counters and column-sum
+// scratch, and every buffer is written by one side only between two hand-overs, so the arithmetic
+// and its order are those of the one-stream call: bit-identical results.  aux == main (or null):
+// one stream, hand-overs are no-ops.  Events come from a per-thread pool, recorded again on the
+// next call (a wait already queued is not affected by a later record).
+struct Fork {
+  hipStream_t main, aux;
+  int used = 0;
+  hipError_t err = hipSuccess;
+  Fork(hipStream_t m, hipStream_t a) : main(m), aux(a && a != m ? a : m) {}
+  bool split() const { return aux != main; }
+  hipEvent_t next() {
+    thread_local std::vector<hipEvent_t> pool;
+    if (used == (int)pool.size()) {
+      hipEvent_t e = nullptr;
+      hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      if (r != hipSuccess) {
+        if (!err) err = r;
+        return nullptr;
+      }
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  void hand(hipStream_t from, hipStream_t to) {  // `to` waits for everything queued on `from` so far
+    if (!split() || err) return;
+    hipEvent_t e = next();
+    if (!e) return;
+    hipError_t r = hipEventRecord(e, from);
+    if (!r) r = hipStreamWaitEvent(to, e, 0);
+    if (r && !err) err = r;
+  }
+  void to_aux() { hand(main, aux); }
+  void to_main() { hand(aux, main); }
+  hipEvent_t mark(hipStream_t from) {  // a point on `from` to wait for later (wait())
+    if (!split() || err) return nullptr;
+    hipEvent_t e = next();
+    if (e) {
+      hipError_t r = hipEventRecord(e, from);
+      if (r && !err) err = r;
+    }
+    return e;
+  }
+  void wait(hipStream_t to, hipEvent_t e) {
+    if (!e || err) return;
+    hipError_t r = hipStreamWaitEvent(to, e, 0);
+    if (r && !err) err = r;
+  }
+};
 
 // ---------------------------------------------------------------------------------------------
 // forward pieces
@@ -731,103 +884,91 @@ __global__ __launch_bounds__(256) void k_tr_atten(int B, int H, const float* __r
   }
 }
 
-// k_tr_atten's rows grouped by image: one workgroup per (image b, group of TS consecutive steps)
-// keeps V_b in registers (thread t owns columns t + 256 j, j < HPT: 49 HPT floats) and VWv_b in LDS,
-// and runs its rows one after another with the next row's small operands (PG, PS rows; S, h, the
-// row's columns) loaded ahead -- V_b and VWv_b are read once per group instead of once per row (2304
-// x 100 KB per training step at B = 128, T = 18), and every row's arithmetic is k_tr_atten's, in the
-// same order (scores by one wave per item, the two softmaxes by wave 0, the context as one fma chain
-// over k per column): bit-identical outputs.
-template <int HPT>
-__global__ __launch_bounds__(256) void k_tr_atten_img(int B, int T, int TS, const float* __restrict__ PG,
-                                                      const float* __restrict__ PS, const float* __restrict__ VWv,
-                                                      const float* __restrict__ Vf, const float* __restrict__ wh,
-                                                      const float* __restrict__ Hs, const float* __restrict__ S,
-                                                      float* __restrict__ alpha, float* __restrict__ beta,
-                                                      float* __restrict__ ctx, float* __restrict__ U) {
-  constexpr int H = 256 * HPT;
-  __shared__ float s_vwv[P * PP], zs[PP], al[PP], sh_b;
-  const int b = blockIdx.x, t0 = blockIdx.y * TS, t1 = t0 + TS < T ? t0 + TS : T;
+// k_tr_atten's rows grouped by image, in three phases instead of a per-row chain: one workgroup of H
+// threads per (image b, group of TS <= 32 consecutive steps).  V_b stays in registers (thread d holds
+// column d: 49 floats), VWv_b and the group's PG / PS rows in LDS.
+//   A: every (row, item) score of the group at once, one per thread: z = w_h . tanh(x) summed by the
+//      same pairing tree as wave_sum's xor butterfly (a[i] += a[i + o], o = 32 .. 1, entries >= 49 zero),
+//      so z is bit-identical to k_tr_atten's wave-cooperative sum, with no cross-lane dependence;
+//   B: the two softmaxes, one wave per row, exactly as k_tr_atten;
+//   C: the context of every row of the group, one fma chain over k per column, and u = c_hat + h.
+// V_b and VWv_b are read once per group instead of once per row (2304 x 100 KB per training step at
+// B = 128, T = 18), and the rows' scores run side by side rather than one wave-reduction at a time:
+// bit-identical outputs to k_tr_atten.
+constexpr int TRA_TS = 32;  // steps per group, at most
+template <int H>
+__global__ __launch_bounds__(H) void k_tr_atten_img(int B, int T, int TS, const float* __restrict__ PG,
+                                                    const float* __restrict__ PS, const float* __restrict__ VWv,
+                                                    const float* __restrict__ Vf, const float* __restrict__ wh,
+                                                    const float* __restrict__ Hs, const float* __restrict__ S,
+                                                    float* __restrict__ alpha, float* __restrict__ beta,
+                                                    float* __restrict__ ctx, float* __restrict__ U) {
+  constexpr int NW = H / 64;
+  __shared__ float s_vwv[P * PP], s_wh[PP], s_pg[TRA_TS][PP], s_ps[TRA_TS][PP], s_z[TRA_TS][PP], s_al[TRA_TS][PP];
+  __shared__ float s_be[TRA_TS];
+  const int b = blockIdx.x, t0 = blockIdx.y * TS, t1 = t0 + TS < T ? t0 + TS : T, n = t1 - t0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t0 >= t1) return;
-  float v[P][HPT];
+  if (n <= 0) return;
+  float v[P];
   const float* vb = Vf + (int64_t)b * P * H;
 #pragma unroll
-  for (int k = 0; k < P; ++k)
+  for (int k = 0; k < P; ++k) v[k] = vb[(int64_t)k * H + t];
+  for (int e = t; e < P * PP; e += H) s_vwv[e] = VWv[(int64_t)b * P * PP + e];
+  if (t < PP) s_wh[t] = t < P ? wh[t] : 0.f;
+  for (int e = t; e < n * PP; e += H) {
+    const int i = e / PP, j = e - i * PP;
+    const int64_t r = (int64_t)(t0 + i) * B + b;
+    s_pg[i][j] = PG[r * PP + j];
+    s_ps[i][j] = PS[r * PP + j];
+  }
+  __syncthreads();
+  // A: scores, one (row, item) per thread
+  for (int q = t; q < n * (P + 1); q += H) {
+    const int i = q / (P + 1), k = q - i * (P + 1);
+    const float* xs = k < P ? &s_vwv[k * PP] : &s_ps[i][0];
+    float a[64];
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) v[k][j] = vb[(int64_t)k * H + t + 256 * j];
-  for (int e = t; e < P * PP; e += 256) s_vwv[e] = VWv[(int64_t)b * P * PP + e];
-  const float whl = lane < P ? wh[lane] : 0.f;
-  // row operands, loaded one row ahead
-  auto ld_small = [&](int r, float& pg, float& ps) {
-    pg = lane < P ? PG[(int64_t)r * PP + lane] : 0.f;
-    ps = lane < P ? PS[(int64_t)r * PP + lane] : 0.f;
-  };
-  auto ld_cols = [&](int r, float (&sv)[HPT], float (&hv)[HPT]) {
+    for (int j = 0; j < 64; ++j) a[j] = j < P ? s_wh[j] * tanhf(xs[j] + s_pg[i][j]) : 0.f;
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) {
-      sv[j] = S[(int64_t)r * H + t + 256 * j];
-      hv[j] = Hs[(int64_t)r * H + t + 256 * j];
-    }
-  };
-  float pg, ps, sv[HPT], hv[HPT];
-  ld_small(t0 * B + b, pg, ps);
-  ld_cols(t0 * B + b, sv, hv);
-  __syncthreads();  // s_vwv
-  for (int st = t0; st < t1; ++st) {
-    const int r = st * B + b;
-    for (int k = w; k <= P; k += 4) {
-      float z = 0.f;
-      if (lane < P) {
-        const float x = (k < P ? s_vwv[k * PP + lane] : ps) + pg;
-        z = whl * tanhf(x);
-      }
-      z = wave_sum(z);
-      if (lane == 0) zs[k] = z;
-    }
-    __syncthreads();
-    if (w == 0) {
-      const float z = lane < P ? zs[lane] : -INFINITY;
-      const float m = wave_max(z);
-      const float e = lane < P ? expf(z - m) : 0.f;
-      const float a = e / wave_sum(e);
-      if (lane < P) {
-        al[lane] = a;
-        alpha[(int64_t)r * PP + lane] = a;
-      }
-      const float zsn = zs[P];
-      const float m2 = fmaxf(m, zsn);
-      const float e2 = lane < P ? expf(z - m2) : 0.f;
-      const float es = expf(zsn - m2);
-      const float S2 = wave_sum(e2) + es;
-      if (lane == 0) {
-        sh_b = es / S2;
-        beta[r] = es / S2;
-      }
-    }
-    __syncthreads();
-    const float be = sh_b;
-    float svc[HPT], hvc[HPT];
+    for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) {
-      svc[j] = sv[j];
-      hvc[j] = hv[j];
+      for (int j = 0; j < o; ++j) a[j] = a[j] + a[j + o];
+    s_z[i][k] = a[0];
+  }
+  __syncthreads();
+  // B: softmax_49 (alpha) and softmax_50 (beta = its last entry), one wave per row
+  for (int i = w; i < n; i += NW) {
+    const int64_t r = (int64_t)(t0 + i) * B + b;
+    const float z = lane < P ? s_z[i][lane] : -INFINITY;
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float al = e / wave_sum(e);
+    if (lane < P) {
+      s_al[i][lane] = al;
+      alpha[r * PP + lane] = al;
     }
-    if (st + 1 < t1) {  // the next row's operands, in flight under this row's context
-      ld_small(r + B, pg, ps);
-      ld_cols(r + B, sv, hv);
+    const float zsn = s_z[i][P];
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      s_be[i] = es / S2;
+      beta[r] = es / S2;
     }
+  }
+  __syncthreads();
+  // C: context and u for every row of the group (column t)
+  for (int i = 0; i < n; ++i) {
+    const int64_t r = (int64_t)(t0 + i) * B + b;
+    const float sv = S[r * H + t], hv = Hs[r * H + t];
+    float c = 0.f;
 #pragma unroll
-    for (int j = 0; j < HPT; ++j) {
-      const int d = t + 256 * j;
-      float c = 0.f;
-#pragma unroll
-      for (int k = 0; k < P; ++k) c = __builtin_fmaf(al[k], v[k][j], c);
-      ctx[(int64_t)r * H + d] = c;
-      const float chat = be * svc[j] + (1.f - be) * c;
-      U[(int64_t)r * H + d] = chat + hvc[j];
-    }
-    __syncthreads();  // al / sh_b / zs are rewritten by the next row
+    for (int k = 0; k < P; ++k) c = __builtin_fmaf(s_al[i][k], v[k], c);
+    ctx[r * H + t] = c;
+    const float be = s_be[i];
+    const float chat = be * sv + (1.f - be) * c;
+    U[r * H + t] = chat + hv;
   }
 }
 
@@ -1396,6 +1537,7 @@ struct TrainWS {
   int* prow;
   // backward scratch
   float *Up, *dU, *dS, *dPG, *dPS, *dV, *dVWv, *dwh, *dH, *dC, *dG, *DG, *dX, *dh_rec, *dc_rec, *dvg, *csum, *gsplit, *dsp;
+  float *gsplit2, *csum2;  // the aux stream's split-K and column-sum scratch (Fork)
   float *dA, *dag;  // d(features) pieces: through V [B*49][C] and through a_g [B][C]
   float *dz, *dwr;  // per-row dz and w_h-gradient terms of k_tr_atb_row, summed per image by k_tr_atb_img
   // bf16 operands of the large GEMMs (AA_TRAIN_BF16, k_bgemm): U_p, W_m, dS (rows), W_m^T, dS^T, U_p^T,
@@ -1404,6 +1546,7 @@ struct TrainWS {
   // fused recurrent steps (bf16): W_hh as forward / backward B-fragments, h_t and DG_t ping-pong bf16 copies
   bf16x8 *whf, *whb;
   __bf16 *hb[2], *dgb[2];
+  int* tcnt;  // split-K arrival counters (splitk_last), 2 x TR_CNT (main, aux): zeroed by the forward's first kernel
   int *trank, *tcount, *torder, *tsmall;
 };
 
@@ -1463,6 +1606,8 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
   w.csum = c.take<float>((size_t)CS_CH * (d.vocab > 4 * H ? d.vocab : 4 * H));
   w.trank = c.take<int>(R);
   w.gsplit = c.take<float>(TR_SPLIT_FLOATS);
+  w.gsplit2 = c.take<float>(TR_SPLIT_FLOATS);
+  w.csum2 = c.take<float>((size_t)CS_CH * (d.vocab > 4 * H ? d.vocab : 4 * H));
   w.dsp = c.take<float>(R * (size_t)((d.vocab + 63) / 64 * 64));
   w.tcount = c.take<int>(R);
   w.torder = c.take<int>(R);
@@ -1487,6 +1632,7 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
       w.hb[i] = c.take<__bf16>((size_t)B * H);
       w.dgb[i] = c.take<__bf16>((size_t)B * 4 * H);
     }
+    w.tcnt = c.take<int>(2 * TR_CNT);
   }
   *bytes = c.off;
   return w;
@@ -1512,12 +1658,13 @@ static inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs
 // Decoder.forward over T teacher-forced steps (baseline_attention.py:148-194 with the adaptive
 // block, adaptive_attention.py:110-134) from V, v_g, (h0, c0) already in the workspace: every
 // activation of the T steps (Hs, Cs, S, alpha, beta, U = c_hat + h, ...) lands in ws, t-major.
+// V and VWv = V W_v^T are the caller's: `join` (if set) makes the stream wait for them right before
+// the attention, the first kernel that reads them.
 static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const TrainWS& s, const aa_dims& d, int B,
-                         int T, const int64_t* tokens, int tok_ld) {
+                         int T, const int64_t* tokens, int tok_ld, Fork* join = nullptr) {
   using namespace aa;
   const int H = d.hidden, E = d.embed, V = d.vocab, R = T * B;
   const hipStream_t st = gc.s;
-  tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   // x_t and the step-invariant input terms for all steps
   hipLaunchKernelGGL(k_tr_x, dim3(R), dim3(256), 0, st, tokens, tok_ld, w->embed_w, V, E, s.vg, B, T, s.X);
   tgemm(gc, R, 4 * H, 2 * E, s.X, 2 * E, 0, w->lstm_w_ih, 2 * E, 0, s.PRE, 5 * H, 0, w->lstm_b_ih, w->lstm_b_hh);
@@ -1565,21 +1712,30 @@ static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const Train
   // attention projections and the attention itself (adaptive_attention.py:26-58)
   tgemm(gc, R, P, H, s.Hs, H, 0, w->att_affine_g_w, H, 0, s.PG, PP);
   tgemm(gc, R, P, H, s.S, H, 0, w->att_affine_s_w, H, 0, s.PS, PP);
-  {
+  if (join) join->to_main();
+  static const bool tra_row = [] {  // AA_TRA_ROW=1: the per-row k_tr_atten (bitwise A/B of the two forms)
+    const char* e = getenv("AA_TRA_ROW");
+    return e && atoi(e) == 1;
+  }();
+  if (tra_row) {
+    hipLaunchKernelGGL(k_tr_atten, dim3(R), dim3(256), 0, st, B, H, s.PG, s.PS, s.VWv, s.V, w->att_affine_h_w, s.Hs,
+                       s.S, s.alpha, s.beta, s.ctx, s.U);
+  } else {
     // rows grouped by image (V_b read once per group): groups of TS steps so that the grid covers
     // the chip (>= 256 workgroups when B is small)
     int G = B > 0 ? (256 + B - 1) / B : 1;
     G = G < T ? G : T;
+    G = G > (T + TRA_TS - 1) / TRA_TS ? G : (T + TRA_TS - 1) / TRA_TS;  // at most TRA_TS steps per group
     const int TS = (T + G - 1) / G;
     G = (T + TS - 1) / TS;
-#define AA_TRA(HPT_)                                                                                              \
-  hipLaunchKernelGGL(k_tr_atten_img<HPT_>, dim3(B, G), dim3(256), 0, st, B, T, TS, s.PG, s.PS, s.VWv, s.V,        \
+#define AA_TRA(H_)                                                                                               \
+  hipLaunchKernelGGL(k_tr_atten_img<H_>, dim3(B, G), dim3(H_), 0, st, B, T, TS, s.PG, s.PS, s.VWv, s.V,          \
                      w->att_affine_h_w, s.Hs, s.S, s.alpha, s.beta, s.ctx, s.U)
     switch (H) {
-      case 256: AA_TRA(1); break;
-      case 512: AA_TRA(2); break;
-      case 768: AA_TRA(3); break;
-      default: AA_TRA(4); break;
+      case 256: AA_TRA(256); break;
+      case 512: AA_TRA(512); break;
+      case 768: AA_TRA(768); break;
+      default: AA_TRA(1024); break;
     }
 #undef AA_TRA
   }
@@ -1588,6 +1744,14 @@ static void decoder_core(const GemmCtx& gc, const aa_ref_weights* w, const Train
 int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
                      const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, float* scores, int32_t N,
                      void* workspace, size_t workspace_bytes, int32_t flags, aa_stream_t stream) {
+  return aa_train_forward_aux(w, dims, feats, B, T, tokens, tok_ld, lengths, scores, N, workspace, workspace_bytes,
+                              flags, stream, nullptr);
+}
+
+int aa_train_forward_aux(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
+                         const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, float* scores, int32_t N,
+                         void* workspace, size_t workspace_bytes, int32_t flags, aa_stream_t stream,
+                         aa_stream_t aux) {
   using namespace aa;
   int rc = train_check(dims, B, T);
   if (rc) return rc;
@@ -1599,24 +1763,35 @@ int aa_train_forward(const aa_ref_weights* w, const aa_dims* dims, const float* 
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
-  // encoder tail (baseline_attention.py:46-60), reference weight layouts
+  Fork f(st, (hipStream_t)aux);
+  const bool bf = (flags & AA_TRAIN_BF16) != 0;
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt)};
+  const GemmCtx ga{f.aux, s.gsplit2, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt + TR_CNT)};
+  // encoder tail (baseline_attention.py:46-60), reference weight layouts: a_g and the heads on the
+  // main stream (the LSTM needs them), the spatial V = relu(A W_a^T + b) and VWv on aux beside the
+  // LSTM (the attention is their first reader)
   if (gc.bf16 && H % 64 == 0 && C % 64 == 0) {
-    // bf16 step: V = relu(A W_a^T + b) on k_bgemm; one pass over the feature map packs both bf16
-    // operand layouts (this GEMM's rows, the backward's dW_a columns) and computes a_g
-    hipLaunchKernelGGL(k_pk_feats3, dim3(C / 64, B), dim3(256), 0, st, feats, B, C, s.ftT, s.ftC, rup64(B * P), s.a_g);
-    pk_rows(st, w->enc_affine_a_w, C, nullptr, H, C, s.wmT, C);
-    bgemm(gc, B * P, H, C, s.ftT, C, s.wmT, C, s.V, H, w->enc_affine_a_b, nullptr, 0, 1);
+    // bf16 step: V on k_bgemm; one pass over the feature map packs both bf16 operand layouts (this
+    // GEMM's rows, the backward's dW_a columns) and computes a_g
+    hipLaunchKernelGGL(k_pk_feats3, dim3(C / 64, B), dim3(256), 0, st, feats, B, C, s.ftT, s.ftC, rup64(B * P), s.a_g,
+                       s.tcnt, 2 * TR_CNT);
+    f.to_aux();
+    pk_rows(ga.s, w->enc_affine_a_w, C, nullptr, H, C, s.wmT, C);
+    bgemm(ga, B * P, H, C, s.ftT, C, s.wmT, C, s.V, H, w->enc_affine_a_b, nullptr, 0, 1);
   } else {
+    AA_TRY(hipMemsetAsync(s.tcnt, 0, sizeof(int) * 2 * TR_CNT, st));
     hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
+    f.to_aux();
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
-    hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, st, feats, B, C, H, w->enc_affine_a_w,
+    hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, ga.s, feats, B, C, H, w->enc_affine_a_w,
                        w->enc_affine_a_b, s.V);
   }
+  tgemm(ga, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   tgemm(gc, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
-  decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
+  decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld, &f);
+  if (f.err) return (int)f.err;
   // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
   hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
   if (gc.bf16 && H % 64 == 0) {
@@ -1669,13 +1844,15 @@ int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, const float
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, Vc = dims->vocab, R = T * B;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0, splitk_counters(s.tcnt)};
   hipError_t e = hipSuccess;
   if (!e) e = hipMemcpyAsync(s.V, V, sizeof(float) * (size_t)B * P * H, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.vg, v_g, sizeof(float) * (size_t)B * E, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.h0, h0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.c0, c0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
+  if (!e) e = hipMemsetAsync(s.tcnt, 0, sizeof(int) * 2 * TR_CNT, st);  // split-K arrival counters
   if (e) return (int)e;
+  tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
   if (scores) {  // mlp(c_hat + h) for every (b, t), batch-first (:132)
     hipLaunchKernelGGL(k_bt_rowmap, dim3(nblk(R)), dim3(256), 0, st, B, T, s.prow);
@@ -1696,6 +1873,14 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
                       const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, const float* dscores, int32_t N,
                       const aa_ref_grads* grads, float* dfeats, void* workspace, size_t workspace_bytes,
                       int32_t flags, aa_stream_t stream) {
+  return aa_train_backward_aux(w, dims, feats, B, T, tokens, tok_ld, lengths, dscores, N, grads, dfeats, workspace,
+                               workspace_bytes, flags, stream, nullptr);
+}
+
+int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B, int32_t T,
+                          const int64_t* tokens, int32_t tok_ld, const int32_t* lengths, const float* dscores,
+                          int32_t N, const aa_ref_grads* grads, float* dfeats, void* workspace, size_t workspace_bytes,
+                          int32_t flags, aa_stream_t stream, aa_stream_t aux) {
   using namespace aa;
   int rc = train_check(dims, B, T);
   if (rc) return rc;
@@ -1707,9 +1892,24 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, C = dims->channels, V = dims->vocab, R = T * B, E2 = 2 * E;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
+  Fork f(st, (hipStream_t)aux);
+  const hipStream_t sa = f.aux;
+  const bool bf = (flags & AA_TRAIN_BF16) != 0;
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt)};
+  const GemmCtx ga{sa, s.gsplit2, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt + TR_CNT)};
 #define GRAD(f) (grads->f)
   const size_t RH = (size_t)R * H;
+  // Streams (Fork): main = dscores -> dU -> attention backward -> sentinel -> LSTM through time ->
+  // dx -> embedding / encoder-head gradients; aux = the weight gradients hanging off that chain
+  // (dW_m, dW_g / dW_s / dW_v / the V-side encoder, dW_x / dW_h, dW_hh / dW_ih / b_ih) and the token
+  // ranking of the embedding gradient.
+  f.to_aux();
+  // x_t = [embed(tok); v_g] (baseline_attention.py:151-154): the tokens' segmented-sum order
+  AA_TRY(hipMemsetAsync(GRAD(embed_w), 0, sizeof(float) * (size_t)V * E, sa));
+  hipLaunchKernelGGL(k_tok_rank, dim3((R + 3) / 4), dim3(256), 0, sa, tokens, tok_ld, B, R, V, s.trank, s.tcount,
+                     s.tsmall);
+  hipLaunchKernelGGL(k_tok_place, dim3(nblk(R)), dim3(256), 0, sa, R, s.trank, s.tsmall, s.torder);
+  hipEvent_t tok_done = f.mark(sa);
   // mlp (adaptive_attention.py:132): dU[prow] = dS W_m; dW_m = dS^T U_p; db_m = colsum(dS)
   const int Vp = (V + 63) / 64 * 64;  // dscores re-pitched to whole 16-B rows for vector loads
   const bool bg = gc.bf16 && H % 64 == 0;  // the large GEMMs on k_bgemm
@@ -1725,16 +1925,17 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   // / dPS before the attention backward accumulates into them)
   AA_TRY(hipMemsetAsync(s.dU, 0, (size_t)((char*)(s.dPS + (size_t)R * PP) - (char*)s.dU), st));
   hipLaunchKernelGGL(k_gather_rows, dim3(nblk((int64_t)N * H)), dim3(256), 0, st, s.U, s.prow, N, H, s.Up);
+  f.to_aux();  // dW_m on aux
   if (bg) {
     const int Kv = Vp, Kn = rup64(N);                                     // dS as bf16 [N][Vp]: k_pad_rows
+    pk_trans(sa, s.dspb, Vp, N, V, s.dspT, Kn);                            // dS^T [V][Kn]
+    pk_trans(sa, s.Up, H, N, H, s.upT, Kn);                                // U_p^T [H][Kn]
+    bgemm(ga, V, H, Kn, s.dspT, Kn, s.upT, Kn, GRAD(mlp_w), H);            // dW_m = dS^T U_p
     pk_trans(st, w->mlp_w, H, V, H, s.wmT, Kv);                            // W_m^T [H][Kv]
     bgemm(gc, N, H, Kv, s.dspb, Kv, s.wmT, Kv, s.dU, H, nullptr, s.prow);  // dU[prow] = dS W_m
-    pk_trans(st, s.dspb, Vp, N, V, s.dspT, Kn);                            // dS^T [V][Kn]
-    pk_trans(st, s.Up, H, N, H, s.upT, Kn);                                // U_p^T [H][Kn]
-    bgemm(gc, V, H, Kn, s.dspT, Kn, s.upT, Kn, GRAD(mlp_w), H);            // dW_m = dS^T U_p
   } else {
+    tgemm(ga, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
     tgemm(gc, N, H, V, s.dsp, Vp, 0, w->mlp_w, H, 1, s.dU, H, 0, nullptr, nullptr, 0, nullptr, s.prow);
-    tgemm(gc, V, H, N, s.dsp, Vp, 1, s.Up, H, 1, GRAD(mlp_w), H);
   }
   if (bg) hipLaunchKernelGGL(k_colsum_fin, dim3((V + 255) / 256), dim3(256), 0, st, s.csum, V, GRAD(mlp_b));
   else colsum(st, s.dsp, N, V, (int64_t)Vp, s.csum, GRAD(mlp_b));
@@ -1754,18 +1955,32 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   }
 #undef AA_ATB
   // dH = dU (u = c_hat + h) was written by k_tr_atb_row
+  f.to_aux();  // the attention's weight gradients and the V side of the encoder on aux
   tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
-  tgemm(gc, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
   tgemm(gc, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
-  tgemm(gc, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
-  tgemm(gc, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
-  tgemm(gc, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
-  hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(256), 0, st, s.dwh, B, GRAD(att_affine_h_w));
+  tgemm(ga, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
+  tgemm(ga, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
+  tgemm(ga, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
+  tgemm(ga, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
+  hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(256), 0, sa, s.dwh, B, GRAD(att_affine_h_w));
+  // encoder V = relu(A W_a^T + b) (baseline_attention.py:46-51)
+  hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, sa, s.dV, s.V, (int64_t)B * P * H);
+  if (gc.bf16 && H % 64 == 0) {  // dW_a = dV^T A
+    const int Kb = rup64(B * P);
+    pk_trans(sa, s.dV, H, B * P, H, s.dvT, Kb);
+    // the feature map's [C][Kb] bf16 operand was packed by the forward (k_pk_feats3, same workspace)
+    bgemm(ga, H, C, Kb, s.dvT, Kb, s.ftC, Kb, GRAD(enc_affine_a_w), C);
+  } else {
+    tgemm(ga, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);              // dW_a = dV^T A
+  }
+  colsum(sa, s.dV, B * P, H, (int64_t)H, s.csum2, GRAD(enc_affine_a_b));
+  if (dfeats) tgemm(ga, B * P, C, H, s.dV, H, 0, w->enc_affine_a_w, C, 1, s.dA, C);      // dA = dV W_a
   // Sentinel backward (:79-83): h_{t-1} input = Hs[r - B] for r >= B, 0 for t = 0
   hipLaunchKernelGGL(k_tr_sent_bwd, dim3(nblk((int64_t)RH)), dim3(256), 0, st, s.dS, s.SG, s.Cs, s.dG, s.dC,
                      (int64_t)RH);
-  tgemm(gc, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
-  tgemm(gc, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
+  f.to_aux();
+  tgemm(ga, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
+  tgemm(ga, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
   tgemm(gc, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
   tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
   // LSTM backward through time (baseline_attention.py:167-178)
@@ -1778,15 +1993,15 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
     for (int t = T - 1; t >= 0; --t) {
       const size_t o = (size_t)t * B * H;
       const float* cp = t ? s.Cs + o - (size_t)B * H : s.c0;
-      const float* ga = s.GA + (size_t)t * B * 4 * H;
+      const float* ga4 = s.GA + (size_t)t * B * 4 * H;
       float* dg = s.DG + (size_t)t * B * 4 * H;
 #define AA_LB(H_)                                                                                                   \
   if (t == T - 1)                                                                                                   \
     hipLaunchKernelGGL((k_tr_lstm_b<H_, true>), dim3(grid), dim3(256), 0, st, B, (const __bf16*)nullptr, s.whb,     \
-                       s.dH + o, s.dC + o, s.dc_rec, ga, s.Cs + o, cp, dg, s.dgb[t & 1]);                           \
+                       s.dH + o, s.dC + o, s.dc_rec, ga4, s.Cs + o, cp, dg, s.dgb[t & 1]);                          \
   else                                                                                                              \
     hipLaunchKernelGGL((k_tr_lstm_b<H_, false>), dim3(grid), dim3(256), 0, st, B, (const __bf16*)s.dgb[(t + 1) & 1], \
-                       s.whb, s.dH + o, s.dC + o, s.dc_rec, ga, s.Cs + o, cp, dg, s.dgb[t & 1])
+                       s.whb, s.dH + o, s.dC + o, s.dc_rec, ga4, s.Cs + o, cp, dg, s.dgb[t & 1])
       switch (H) {
         case 256: AA_LB(256); break;
         case 512: AA_LB(512); break;
@@ -1795,6 +2010,7 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
       }
 #undef AA_LB
     }
+    f.to_aux();  // DG complete: the LSTM weight gradients on aux
     tgemm(gc, B, H, 4 * H, s.DG, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);
   } else {
     int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
@@ -1808,22 +2024,20 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
       S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H, 0, nullptr,
                 nullptr, 0, nullptr, nullptr, t > 0);
     }
+    f.to_aux();
   }
-  tgemm(gc, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
-  tgemm(gc, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);
-  tgemm(gc, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
-  colsum(st, s.DG, R, 4 * H, (int64_t)4 * H, s.csum, GRAD(lstm_b_ih));
-  AA_TRY(hipMemcpyAsync(GRAD(lstm_b_hh), GRAD(lstm_b_ih), sizeof(float) * 4 * H, hipMemcpyDeviceToDevice, st));
+  tgemm(ga, 4 * H, H, B, s.DG, 4 * H, 1, s.h0, H, 1, GRAD(lstm_w_hh), H);                 // t = 0: h_{-1} = h0
+  tgemm(ga, 4 * H, H, R - B, s.DG + (size_t)B * 4 * H, 4 * H, 1, s.Hs, H, 1, GRAD(lstm_w_hh), H, 1);
+  tgemm(ga, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
+  colsum(sa, s.DG, R, 4 * H, (int64_t)4 * H, s.csum2, GRAD(lstm_b_ih));
+  AA_TRY(hipMemcpyAsync(GRAD(lstm_b_hh), GRAD(lstm_b_ih), sizeof(float) * 4 * H, hipMemcpyDeviceToDevice, sa));
   tgemm(gc, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
   // x_t = [embed(tok); v_g] (baseline_attention.py:151-154)
-  AA_TRY(hipMemsetAsync(GRAD(embed_w), 0, sizeof(float) * (size_t)V * E, st));
-  hipLaunchKernelGGL(k_tok_rank, dim3((R + 3) / 4), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.trank, s.tcount,
-                     s.tsmall);
-  hipLaunchKernelGGL(k_tok_place, dim3(nblk(R)), dim3(256), 0, st, R, s.trank, s.tsmall, s.torder);
+  f.wait(st, tok_done);
   hipLaunchKernelGGL(k_tr_embed_bwd, dim3(R), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.torder, s.trank, s.tcount,
                      s.dX, E, GRAD(embed_w));
   hipLaunchKernelGGL(k_tr_vg_bwd, dim3(nblk((int64_t)B * E)), dim3(256), 0, st, s.dX, s.vg, B, T, E, s.dvg);
-  // encoder tail (baseline_attention.py:46-60)
+  // encoder heads (baseline_attention.py:52-60)
   tgemm(gc, E, C, B, s.dvg, E, 1, s.a_g, C, 1, GRAD(enc_affine_b_w), C);
   colsum(st, s.dvg, B, E, (int64_t)E, s.csum, GRAD(enc_affine_b_b));
   hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)B * H);
@@ -1832,23 +2046,15 @@ int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const float*
   colsum(st, s.dh_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_h0_b));
   tgemm(gc, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);
   colsum(st, s.dc_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_c0_b));
-  hipLaunchKernelGGL(k_relu_mask, dim3(nblk((int64_t)B * P * H)), dim3(256), 0, st, s.dV, s.V, (int64_t)B * P * H);
-  if (gc.bf16 && H % 64 == 0) {  // dW_a = dV^T A
-    const int Kb = rup64(B * P);
-    pk_trans(st, s.dV, H, B * P, H, s.dvT, Kb);
-    // the feature map's [C][Kb] bf16 operand was packed by the forward (k_pk_feats3, same workspace)
-    bgemm(gc, H, C, Kb, s.dvT, Kb, s.ftC, Kb, GRAD(enc_affine_a_w), C);
-  } else {
-    tgemm(gc, H, C, B * P, s.dV, H, 1, feats, C, 2, GRAD(enc_affine_a_w), C);              // dW_a = dV^T A
-  }
-  colsum(st, s.dV, B * P, H, (int64_t)H, s.csum, GRAD(enc_affine_a_b));
   if (dfeats) {  // gradient into the trunk's output A (CNN fine-tuning, train.py:89)
-    tgemm(gc, B * P, C, H, s.dV, H, 0, w->enc_affine_a_w, C, 1, s.dA, C);              // dA = dV W_a
     tgemm(gc, B, C, E, s.dvg, E, 0, w->enc_affine_b_w, C, 1, s.dag, C);                // d a_g = dv_g W_b
     tgemm(gc, B, C, H, s.dh_rec, H, 0, w->enc_affine_h0_w, C, 1, s.dag, C, 1);         //   + dh0 W_h0
     tgemm(gc, B, C, H, s.dc_rec, H, 0, w->enc_affine_c0_w, C, 1, s.dag, C, 1);         //   + dc0 W_c0
-    hipLaunchKernelGGL(k_dfeats, dim3((C + 63) / 64, B), dim3(256), 0, st, s.dA, s.dag, C, dfeats);
   }
+  f.to_main();  // everything on aux (dA above) is done before the call's work ends on main
+  if (dfeats)
+    hipLaunchKernelGGL(k_dfeats, dim3((C + 63) / 64, B), dim3(256), 0, st, s.dA, s.dag, C, dfeats);
+  if (f.err) return (int)f.err;
 #undef GRAD
   return aa_launch_status();
 }

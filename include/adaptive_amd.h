@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AA_ABI_VERSION 15
+#define AA_ABI_VERSION 16
 #define AA_API __attribute__((visibility("default")))
 
 /* error codes (negative); positive codes are hipError_t values */
@@ -246,6 +246,21 @@ AA_API int aa_train_backward(const aa_ref_weights* w, const aa_dims* dims, const
                              const int32_t* lengths, const float* dscores, int32_t N,
                              const aa_ref_grads* grads, float* dfeats, void* workspace,
                              size_t workspace_bytes, int32_t flags, aa_stream_t stream);
+/* The same two calls with a second stream `aux` (another stream of the same device, or NULL = one
+ * stream): the work off the step's dependency chain -- the encoder's spatial V GEMM beside the LSTM
+ * forward, the weight gradients beside the LSTM backward -- runs on aux, handed over by events.
+ * Results are bit-identical to the one-stream calls (same kernels, same arithmetic order); both
+ * calls end with `stream` waiting for everything they queued on aux, so the caller orders only
+ * against `stream`.  aux must not be used by anything else during a call. */
+AA_API int aa_train_forward_aux(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B,
+                                int32_t T, const int64_t* tokens, int32_t tok_ld, const int32_t* lengths,
+                                float* scores, int32_t N, void* workspace, size_t workspace_bytes, int32_t flags,
+                                aa_stream_t stream, aa_stream_t aux);
+AA_API int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const float* feats, int32_t B,
+                                 int32_t T, const int64_t* tokens, int32_t tok_ld, const int32_t* lengths,
+                                 const float* dscores, int32_t N, const aa_ref_grads* grads, float* dfeats,
+                                 void* workspace, size_t workspace_bytes, int32_t flags, aa_stream_t stream,
+                                 aa_stream_t aux);
 
 /* ---- Decoder.forward over T > 1 teacher-forced steps -------------------------------------------
  * decoder(V, v_g, captions, states) (baseline_attention.py:148-194 with the adaptive block,

@@ -130,6 +130,30 @@ def test_train_step_deterministic(gpu_device):
         assert torch.equal(grads[0][k], grads[1][k]), k
 
 
+@pytest.mark.parametrize("bf16", [True, False])
+def test_train_two_streams_bit_identical_to_one(gpu_device, bf16):
+    """aa_train_forward_aux / aa_train_backward_aux (the V GEMM and the weight gradients on a second
+    stream) against the one-stream calls: scores, every gradient and dL/dfeats bit for bit, on
+    bench_train's B = 128, T = 18 batch (lengths T .. T/2)."""
+    from bench_train import make_batch
+    from adaptive_amd.adaptive_attention import synthetic_features
+    caps_np, lengths = make_batch(128, 18)
+    caps = torch.from_numpy(caps_np).to(gpu_device)
+    out = []
+    for two in (True, False):
+        model = _model(gpu_device)
+        model.train_bf16 = bf16
+        model.train_aux_stream = two
+        feats = synthetic_features(128, gpu_device, seed=3).requires_grad_(True)
+        loss, packed = _loss(model, feats, caps, lengths)
+        loss.backward()
+        got = {k: p.grad.clone() for k, p in model.named_parameters()}
+        got["scores"], got["dfeats"] = packed[0].detach().clone(), feats.grad.clone()
+        out.append(got)
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+
+
 def test_train_closure_adam_clip_reduces_loss(gpu_device):
     """train.py:197-219 as written: zero_grad, forward, CE, backward, clip LSTM grad norm, Adam step."""
     B, L = 8, 10

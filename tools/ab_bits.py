@@ -26,6 +26,7 @@ def dump_train(path, batch, T, dtype):
     caps_np, lengths = make_batch(batch, T)
     m = Encoder2Decoder(Config()).to(dev).load_synthetic(123)
     m.train_bf16 = dtype == "bf16"
+    m.train_aux_stream = os.environ.get("AB_ONE_STREAM") != "1"  # bitwise A/B of the two-stream calls
     feats = synthetic_features(batch, dev, seed=0)
     caps = torch.from_numpy(caps_np).to(dev)
     packed = m(feats, caps, lengths)

@@ -26,7 +26,7 @@ for s in $steps; do
     prof)  step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-eval-loop --pipeline-depth 1 --steps 20 > $out/prof.log 2>&1
            f=$(find $out/prof -name '*kernel_stats.csv' | head -1); head -14 "$f" | cut -c1-160 ;;
     train) step train timeout -k 10 300 python bench_train.py --no-cpu-baseline > $out/train_bench.json 2> $out/train_bench.err
-           python3 -c "import json;a=json.load(open('$out/train_bench.json'));print('train', round(a['value'],1), 'steps/s')" ;;
+           python3 -c "import json;a=json.load(open('$out/train_bench.json'));print('train', round(a['value'],1), 'steps/s', 'ms', round(a['ms_per_step'],3), 'host ms', round(a.get('host_ms_per_step',0),3))" ;;
     trainprof) step trainprof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_train -o run --output-format csv -- python3 bench_train.py --no-cpu-baseline --steps 10 > $out/prof_train.log 2>&1
            f=$(find $out/prof_train -name '*kernel_stats.csv' | head -1); head -12 "$f" | cut -c1-140 ;;
     ab) # A/B of an environment switch: AB_VAR=name (values 0 / 1), two interleaved rounds of short bench runs
@@ -35,11 +35,26 @@ for s in $steps; do
              echo "[ab $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
              python3 -c "import json;d=json.load(open('$out/ab$v.$r.json'));k=d['kernels'];print('${AB_VAR:-AA_ENC_REMAP}=$v', round(d['value']), 'pipe', round(d['pipelined']['value']), {n: round(e['avg_ms']*1e3,2) for n,e in k.items()})"
            done; done ;;
+    trainab) # A/B of an environment switch on the training bench: AB_VAR=name (0 / 1), two interleaved rounds
+           for r in 1 2; do for v in 0 1; do
+             env ${AB_VAR:-AA_SPLITK_REDUCE}=$v timeout -k 10 300 python bench_train.py --no-cpu-baseline > $out/trainab$v.$r.json 2>> $out/trainab.err; rc=$?
+             echo "[trainab $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
+             python3 -c "import json;a=json.load(open('$out/trainab$v.$r.json'));print('${AB_VAR:-AA_SPLITK_REDUCE}=$v train', round(a['value'],1), 'steps/s host ms', round(a.get('host_ms_per_step',0),3))"
+           done; done ;;
     pipe) # pipelined-rate probe: depth 2/3/4 x slot streams raw/aux
            for ps in x; do for d in 2 3 4; do
              timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval-loop --no-trace --steps 20 --pipeline-depth $d > $out/pipe_${ps}_$d.json 2>> $out/pipe.err; rc=$?
              echo "[pipe $ps $d] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
              python3 -c "import json;d=json.load(open('$out/pipe_${ps}_$d.json'));print('streams $ps depth $d seq', round(d['value']), 'pipe', round(d['pipelined']['value']))"
+           done; done ;;
+    bits) # bitwise A/B of env switches on one training step (each switch: value 1 vs 0), bf16 and fp32
+           for var in ${BITS_VARS:-AA_TRA_ROW AA_SPLITK_REDUCE}; do for dt in bf16 fp32; do
+             for v in 1 0; do
+               env $var=$v timeout -k 10 300 python tools/ab_bits.py dump /tmp/bits_${var}_${dt}_$v.npz --train $dt --batch 128 --T 18 > $out/bits_${var}_$v.log 2>&1; rc=$?
+               echo "[bits $var $dt $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
+             done
+             echo "== $var $dt"; python tools/ab_bits.py cmp /tmp/bits_${var}_${dt}_1.npz /tmp/bits_${var}_${dt}_0.npz > $out/bits_${var}_${dt}.cmp
+             grep -E "DIFF|ALL BIT" $out/bits_${var}_${dt}.cmp | head -12; rm -f /tmp/bits_${var}_${dt}_*.npz
            done; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
