@@ -47,7 +47,6 @@ struct TG {
   int splits;   // split-K: > 1 -> raw partial tiles to part[split][M][N], reduced by k_tgemm_reduce
   int kper;     // K per split (multiple of the K step)
   float* part;
-  int* cnt;     // split-K with cnt != nullptr: the tile's last-arriving split combines in-launch (splitk_last)
 };
 
 // K step of the training GEMM: 64 with bf16 operands (two 32-wide halves per thread, so a
@@ -76,81 +75,6 @@ __device__ __forceinline__ float sk_sum(const float* __restrict__ src, int S, in
     if (sp < S) v += x[sp];
   for (int sp = SK_MAX; sp < S; ++sp) v += src[sp * MN + i];
   return v + 0.f;
-}
-
-// In-launch split-K combine (k_tgemm, k_bgemm): every split has stored its partial tile; the workgroup
-// that arrives last at the tile's device-scope counter sums the S partials of the tile in split order
-// and applies the epilogue -- exactly k_tgemm_reduce's arithmetic (sk_sum, then bias + bias2, act, row
-// map, accumulate), so the result is bit-identical, one launch (and its boundary) fewer per split
-// GEMM.  Hand-off (the guide's counter recipe in its write-through form): the partials were stored
-// sc1 (store_part: write-through, no release fence -- a per-thread __threadfence() measured 163
-// steps/s against 598, a lane-0 agent release 242: both write the XCD's L2 back), every wave drains
-// them, the workgroup meets at a barrier and lane 0 takes a ticket; the ticket S - 1 is the last
-// arriver, whose lane 0 acquires at agent scope before the workgroup reads the other splits' partials.  The
-// counters start at zero (cleared at the start of each training call) and the last arriver re-zeroes
-// its own.  `flag`: one int of the kernel's own LDS (its staging array, free after the main loop: no
-// second __shared__ object in the kernel).
-// TM x TN tile, 256 threads: thread -> column n0 + (t % TN), rows m0 + t / TN + (256 / TN) q.
-__device__ __forceinline__ void store_part(float* p, float v, bool sc1) {
-  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <int TM, int TN>
-__device__ __forceinline__ void splitk_last(int* flag, int* cnt, int tile, int S, const float* part, int M, int N, int m0, int n0,
-                            float* C, int64_t ldc, const int* crow, const float* bias, const float* bias2, int act,
-                            int accumulate) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    typedef __attribute__((address_space(1))) int gint;  // a global (not flat) agent-scope access
-    gint* c = (gint*)(cnt + tile);
-    const int last = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  constexpr int RS = 256 / TN, NQ = TM / RS, QC = NQ < 4 ? NQ : 4;  // rows in chunks of QC (registers)
-  const int n = n0 + (int)(threadIdx.x % TN), r0 = m0 + (int)(threadIdx.x / TN);
-  if (n >= N) return;
-  const int64_t MN = (int64_t)M * N;
-  const float bv = (bias ? bias[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
-  for (int q0 = 0; q0 < NQ; q0 += QC) {
-    float v[QC];
-#pragma unroll
-    for (int q = 0; q < QC; ++q) v[q] = 0.f;
-    // splits in order; the QC rows of up to 4 splits loaded together
-    for (int sp0 = 0; sp0 < S; sp0 += 4) {
-      float x[4][QC];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < QC; ++q) {
-          const int m = r0 + RS * (q0 + q);
-          x[j][q] = (sp0 + j < S && m < M) ? part[(int64_t)(sp0 + j) * MN + (int64_t)m * N + n] : 0.f;
-        }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (sp0 + j < S)
-#pragma unroll
-          for (int q = 0; q < QC; ++q) v[q] += x[j][q];
-    }
-#pragma unroll
-    for (int q = 0; q < QC; ++q) {
-      const int m = r0 + RS * (q0 + q);
-      if (m >= M) continue;
-      float y = v[q] + 0.f;
-      y += bv;
-      if (act == 1) y = reluf_(y);
-      else if (act == 2) y = tanhf(y);
-      float* dst = C + (int64_t)(crow ? crow[m] : m) * ldc + n;
-      *dst = accumulate ? *dst + y : y;
-    }
-  }
 }
 
 // BF: operands rounded to bf16 (RNE) as they are staged in LDS, products on
@@ -319,11 +243,8 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wmv * 32 + acc_row(r, lane);
-        if (m < g.M) store_part(pt + (int64_t)m * g.N + col, acc[r], g.cnt != nullptr);
+        if (m < g.M) pt[(int64_t)m * g.N + col] = acc[r];
       }
-    if (g.cnt)
-      splitk_last<64, 64>(reinterpret_cast<int*>(&lds[0][0][0]), g.cnt, tile, g.splits, g.part, g.M, g.N, m0, n0, g.C, g.ldc, g.crow, g.bias, g.bias2, g.act,
-                          g.accumulate);
     return;
   }
   if (col >= g.N) return;
@@ -356,16 +277,6 @@ __global__ void k_tgemm_reduce(TG g) {
 // k_tgemm's split-K bound (floats of partials): its split counts, and so its fp32 sums, as before
 // the scratch grew for k_bgemm
 constexpr size_t TG_SPLIT_CAP = (size_t)4 << 20;
-constexpr int TR_CNT = 4096;  // split-K arrival counters (tiles) in a training workspace
-// the in-launch split-K combine (splitk_last) unless AA_SPLITK_REDUCE=1 (the separate k_tgemm_reduce
-// launch: bitwise A/B of the two forms)
-static int* splitk_counters(int* cnt) {
-  static const bool sep = [] {
-    const char* e = getenv("AA_SPLITK_REDUCE");
-    return e && atoi(e) == 1;
-  }();
-  return sep ? nullptr : cnt;
-}
 
 // launch context of a training call: stream + split-K scratch carved from its workspace
 struct GemmCtx {
@@ -373,7 +284,6 @@ struct GemmCtx {
   float* split;
   size_t cap;  // floats
   bool bf16;   // AA_TRAIN_BF16: bf16 operands, fp32 accumulation
-  int* cnt;    // split-K arrival counters (zero between launches): in-launch combine; nullptr = k_tgemm_reduce
 };
 
 // C[M,N] (+)= A W^T style helper with the common cases spelled out at the call sites.  GEMMs with
@@ -407,15 +317,16 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
     kper = ((K + splits - 1) / splits + ks - 1) / ks * ks;
     splits = (K + kper - 1) / kper;
   }
-  // split-K partials combined in-launch by each tile's last split (splitk_last) unless the consumer sums
-  // them itself (defer)
+  // split-K partials reduced by k_tgemm_reduce unless the consumer sums them itself (defer).  (An
+  // in-launch combine by each tile's last-arriving split -- device-scope ticket, write-through
+  // partials -- was bit-identical and measured slower in round 4: 597-602 vs 683-698 steps/s.)
   TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, splits, kper,
-       splits > 1 ? gc.split : nullptr, splits > 1 && !defer && tiles <= TR_CNT ? gc.cnt : nullptr};
+       splits > 1 ? gc.split : nullptr};
   if (gc.bf16)
     hipLaunchKernelGGL(k_tgemm<true>, dim3(tiles * splits), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(k_tgemm<false>, dim3(tiles * splits), dim3(256), 0, s, g);
-  if (splits > 1 && !defer && !g.cnt)
+  if (splits > 1 && !defer)
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
   return splits;
 }
@@ -446,7 +357,6 @@ struct BG {
   int accumulate, splits, kper;
   float* part;
   int act;  // 0 none, 1 relu (after the bias)
-  int* cnt;  // split-K arrival counters: in-launch combine (splitk_last); nullptr = k_tgemm_reduce
 };
 __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BG_T * BG_LD];
@@ -529,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
         const int m = m0 + wm * 64 + x * 32 + acc_row(r, lane);
         if (m >= g.M) continue;
         if (g.splits > 1) {
-          store_part(g.part + (int64_t)split * g.M * g.N + (int64_t)m * g.N + col, acc[x][y][r], g.cnt != nullptr);
+          g.part[(int64_t)split * g.M * g.N + (int64_t)m * g.N + col] = acc[x][y][r];
         } else {
           float v = acc[x][y][r] + bv;
           if (g.act == 1) v = reluf_(v);
@@ -538,9 +448,6 @@ __global__ __launch_bounds__(256, 2) void k_bgemm(BG g) {
         }
       }
   }
-  if (g.splits > 1 && g.cnt)
-    splitk_last<BG_T, BG_T>(reinterpret_cast<int*>(&lds[0][0][0]), g.cnt, tile, g.splits, g.part, g.M, g.N, m0, n0, g.C, g.ldc, g.crow, g.bias, nullptr,
-                            g.act, g.accumulate);
 }
 
 // dst[r][k] = bf16(src[map ? map[r] : r][k]) for k < cols, 0 up to Kp (a multiple of 8): 8 per thread,
@@ -609,11 +516,9 @@ __global__ __launch_bounds__(256) void k_pk_featrows(const float* __restrict__ f
 // k_pk_featrows + the backward's k_pk_feats (three reads of the map, one now).
 __global__ __launch_bounds__(256) void k_pk_feats3(const float* __restrict__ feats, int B, int C,
                                                    __bf16* __restrict__ rows, __bf16* __restrict__ cols, int Kp,
-                                                   float* __restrict__ a_g, int* __restrict__ clr, int nclr) {
+                                                   float* __restrict__ a_g) {
   __shared__ float tile[64 * P];
   const int b = blockIdx.y, c0 = blockIdx.x * 64, t = threadIdx.x;
-  if (blockIdx.x == 0 && blockIdx.y == 0)  // (the training call's split-K arrival counters)
-    for (int i = t; i < nclr; i += 256) clr[i] = 0;
   const float* src = feats + ((int64_t)b * C + c0) * P;
   for (int i = t; i < 64 * P; i += 256) tile[i] = src[i];  // [c][p]
   __syncthreads();
@@ -676,10 +581,9 @@ static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64
   if (splits < 1) splits = 1;
   const int kper = (ksteps + splits - 1) / splits * BG_KS;
   splits = (K + kper - 1) / kper;
-  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr, act,
-             splits > 1 && tiles <= TR_CNT ? gc.cnt : nullptr};
+  const BG g{M, N, K, A, lda, B, ldb, C, ldc, crow, bias, accumulate, splits, kper, splits > 1 ? gc.split : nullptr, act};
   hipLaunchKernelGGL(k_bgemm, dim3(tiles * splits), dim3(256), 0, gc.s, g);
-  if (splits > 1 && !g.cnt) {
+  if (splits > 1) {
     TG r{};
     r.M = M; r.N = N; r.K = K; r.C = C; r.ldc = ldc; r.crow = crow; r.bias = bias; r.accumulate = accumulate;
     r.splits = splits; r.kper = kper; r.part = gc.split; r.act = act;
@@ -1546,7 +1450,6 @@ struct TrainWS {
   // fused recurrent steps (bf16): W_hh as forward / backward B-fragments, h_t and DG_t ping-pong bf16 copies
   bf16x8 *whf, *whb;
   __bf16 *hb[2], *dgb[2];
-  int* tcnt;  // split-K arrival counters (splitk_last), 2 x TR_CNT (main, aux): zeroed by the forward's first kernel
   int *trank, *tcount, *torder, *tsmall;
 };
 
@@ -1632,7 +1535,6 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
       w.hb[i] = c.take<__bf16>((size_t)B * H);
       w.dgb[i] = c.take<__bf16>((size_t)B * 4 * H);
     }
-    w.tcnt = c.take<int>(2 * TR_CNT);
   }
   *bytes = c.off;
   return w;
@@ -1765,21 +1667,19 @@ int aa_train_forward_aux(const aa_ref_weights* w, const aa_dims* dims, const flo
   hipStream_t st = (hipStream_t)stream;
   Fork f(st, (hipStream_t)aux);
   const bool bf = (flags & AA_TRAIN_BF16) != 0;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt)};
-  const GemmCtx ga{f.aux, s.gsplit2, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt + TR_CNT)};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf};
+  const GemmCtx ga{f.aux, s.gsplit2, TR_SPLIT_FLOATS, bf};
   // encoder tail (baseline_attention.py:46-60), reference weight layouts: a_g and the heads on the
   // main stream (the LSTM needs them), the spatial V = relu(A W_a^T + b) and VWv on aux beside the
   // LSTM (the attention is their first reader)
   if (gc.bf16 && H % 64 == 0 && C % 64 == 0) {
     // bf16 step: V on k_bgemm; one pass over the feature map packs both bf16 operand layouts (this
     // GEMM's rows, the backward's dW_a columns) and computes a_g
-    hipLaunchKernelGGL(k_pk_feats3, dim3(C / 64, B), dim3(256), 0, st, feats, B, C, s.ftT, s.ftC, rup64(B * P), s.a_g,
-                       s.tcnt, 2 * TR_CNT);
+    hipLaunchKernelGGL(k_pk_feats3, dim3(C / 64, B), dim3(256), 0, st, feats, B, C, s.ftT, s.ftC, rup64(B * P), s.a_g);
     f.to_aux();
     pk_rows(ga.s, w->enc_affine_a_w, C, nullptr, H, C, s.wmT, C);
     bgemm(ga, B * P, H, C, s.ftT, C, s.wmT, C, s.V, H, w->enc_affine_a_b, nullptr, 0, 1);
   } else {
-    AA_TRY(hipMemsetAsync(s.tcnt, 0, sizeof(int) * 2 * TR_CNT, st));
     hipLaunchKernelGGL(k_avgpool, dim3(nblk((int64_t)B * C)), dim3(256), 0, st, feats, (int64_t)B * C, s.a_g);
     f.to_aux();
     const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
@@ -1787,13 +1687,14 @@ int aa_train_forward_aux(const aa_ref_weights* w, const aa_dims* dims, const flo
                        w->enc_affine_a_b, s.V);
   }
   tgemm(ga, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
+  // the packed rows of the scores (pack_padded_sequence order), also off the chain
+  hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, ga.s, lengths, B, T, s.prow);
   tgemm(gc, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
   decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld, &f);
   if (f.err) return (int)f.err;
   // packed scores = mlp(c_hat + h) on the packed rows (:132, baseline_attention.py:228)
-  hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, st, lengths, B, T, s.prow);
   if (gc.bf16 && H % 64 == 0) {
     pk_rows(st, s.U, H, s.prow, N, H, s.ub, H);
     pk_rows(st, w->mlp_w, H, nullptr, V, H, s.wmb, H);
@@ -1844,13 +1745,12 @@ int aa_decoder_forward(const aa_ref_weights* w, const aa_dims* dims, const float
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const int H = dims->hidden, E = dims->embed, Vc = dims->vocab, R = T * B;
   hipStream_t st = (hipStream_t)stream;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0, splitk_counters(s.tcnt)};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, (flags & AA_TRAIN_BF16) != 0};
   hipError_t e = hipSuccess;
   if (!e) e = hipMemcpyAsync(s.V, V, sizeof(float) * (size_t)B * P * H, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.vg, v_g, sizeof(float) * (size_t)B * E, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.h0, h0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
   if (!e) e = hipMemcpyAsync(s.c0, c0, sizeof(float) * (size_t)B * H, hipMemcpyDeviceToDevice, st);
-  if (!e) e = hipMemsetAsync(s.tcnt, 0, sizeof(int) * 2 * TR_CNT, st);  // split-K arrival counters
   if (e) return (int)e;
   tgemm(gc, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   decoder_core(gc, w, s, *dims, B, T, tokens, tok_ld);
@@ -1895,8 +1795,8 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
   Fork f(st, (hipStream_t)aux);
   const hipStream_t sa = f.aux;
   const bool bf = (flags & AA_TRAIN_BF16) != 0;
-  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt)};
-  const GemmCtx ga{sa, s.gsplit2, TR_SPLIT_FLOATS, bf, splitk_counters(s.tcnt + TR_CNT)};
+  const GemmCtx gc{st, s.gsplit, TR_SPLIT_FLOATS, bf};
+  const GemmCtx ga{sa, s.gsplit2, TR_SPLIT_FLOATS, bf};
 #define GRAD(f) (grads->f)
   const size_t RH = (size_t)R * H;
   // Streams (Fork): main = dscores -> dU -> attention backward -> sentinel -> LSTM through time ->
@@ -2040,8 +1940,12 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
   // encoder heads (baseline_attention.py:52-60)
   tgemm(gc, E, C, B, s.dvg, E, 1, s.a_g, C, 1, GRAD(enc_affine_b_w), C);
   colsum(st, s.dvg, B, E, (int64_t)E, s.csum, GRAD(enc_affine_b_b));
-  hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)B * H);
-  hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dc_rec, s.c0, (int64_t)B * H);
+  if (s.dc_rec == s.dh_rec + (size_t)B * H && s.c0 == s.h0 + (size_t)B * H) {  // carved back to back: one launch
+    hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)2 * B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)2 * B * H);
+  } else {
+    hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dh_rec, s.h0, (int64_t)B * H);
+    hipLaunchKernelGGL(k_tanh_bwd, dim3(nblk((int64_t)B * H)), dim3(256), 0, st, s.dc_rec, s.c0, (int64_t)B * H);
+  }
   tgemm(gc, H, C, B, s.dh_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_h0_w), C);
   colsum(st, s.dh_rec, B, H, (int64_t)H, s.csum, GRAD(enc_affine_h0_b));
   tgemm(gc, H, C, B, s.dc_rec, H, 1, s.a_g, C, 1, GRAD(enc_affine_c0_w), C);

@@ -531,19 +531,27 @@ def main():
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"],
                     "duration_source": f"HIP events ({timing_flags_used()}) on the launch stream around each "
                                        f"launch, traced region"}
+    # k_atten's per-step re-read of V, priced on its own whichever kernel is dominant (k_lstm and
+    # k_atten are within a few per cent of each other)
+    atten_v = None
+    if "k_atten" in kernels:
+        ka = kernels["k_atten"]
+        vb = v_restream_bytes_per_row() * B
+        mall = read_probe(dev, vb)
+        sec = ka["avg_ms"] * 1e-3
+        atten_v = {
+            "bytes_per_launch": vb, "achieved_gbs": vb / sec / 1e9,
+            "mall_read_ceiling_gbs": mall, "frac_of_mall_ceiling": vb / sec / 1e9 / mall,
+            "algorithmic_bytes_per_launch": ka["algorithmic_bytes_per_launch"],
+            "executed_bytes_per_launch": ka["algorithmic_bytes_per_launch"] + vb,
+            "executed_achieved_gbs": (ka["algorithmic_bytes_per_launch"] + vb) / sec / 1e9,
+            "avg_launch_ms": ka["avg_ms"],
+            "note": "k_atten's per-step re-read of V (not algorithmic bytes, SURVEY.md §8d; 51.4 MB at B=512, "
+                    "MALL-resident), priced against the MALL-served read rate of a V-sized buffer "
+                    "measured here (aa_read_probe, re-read back to back)"}
         if dominant == "k_atten":
-            vb = v_restream_bytes_per_row() * B
-            mall = read_probe(dev, vb)
-            sec = kd["avg_ms"] * 1e-3
-            roofline["algorithmic_bytes_per_launch"] = kd["algorithmic_bytes_per_launch"]
-            roofline["v_restream"] = {
-                "bytes_per_launch": vb, "achieved_gbs": vb / sec / 1e9,
-                "mall_read_ceiling_gbs": mall, "frac_of_mall_ceiling": vb / sec / 1e9 / mall,
-                "executed_bytes_per_launch": kd["algorithmic_bytes_per_launch"] + vb,
-                "executed_achieved_gbs": (kd["algorithmic_bytes_per_launch"] + vb) / sec / 1e9,
-                "note": "the per-step re-read of V (not algorithmic bytes, SURVEY.md §8d; 51.4 MB at B=512, "
-                        "MALL-resident), priced against the MALL-served read rate of a V-sized buffer "
-                        "measured here (aa_read_probe, re-read back to back)"}
+            roofline["algorithmic_bytes_per_launch"] = ka["algorithmic_bytes_per_launch"]
+            roofline["v_restream"] = atten_v
 
     ideal = path_ideal_seconds(B, T, v_restream=False)
     ideal_exec = path_ideal_seconds(B, T, v_restream=True)
@@ -604,6 +612,7 @@ def main():
                                  "encoder and LSTM GEMMs run as fp32-accurate bf16x3 MFMA (6 bf16 products, "
                                  "2.67x the fp32 MFMA rate); ids stay bit-identical to the fp32 reference"},
         "roofline": roofline,
+        "atten_v_restream": atten_v,
         "path_roofline": {"bound": "per-kernel", "ideal_ms_per_batch": 1e3 * ideal["total"],
                           "frac": 1e3 * ideal["total"] / ms_per_step,
                           "frac_pipelined": 1e3 * ideal["total"] / (1e3 * elapsed_pipe / K),

@@ -37,9 +37,9 @@ for s in $steps; do
            done; done ;;
     trainab) # A/B of an environment switch on the training bench: AB_VAR=name (0 / 1), two interleaved rounds
            for r in 1 2; do for v in 0 1; do
-             env ${AB_VAR:-AA_SPLITK_REDUCE}=$v timeout -k 10 300 python bench_train.py --no-cpu-baseline > $out/trainab$v.$r.json 2>> $out/trainab.err; rc=$?
+             env ${AB_VAR:-AA_TRA_ROW}=$v timeout -k 10 300 python bench_train.py --no-cpu-baseline > $out/trainab$v.$r.json 2>> $out/trainab.err; rc=$?
              echo "[trainab $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
-             python3 -c "import json;a=json.load(open('$out/trainab$v.$r.json'));print('${AB_VAR:-AA_SPLITK_REDUCE}=$v train', round(a['value'],1), 'steps/s host ms', round(a.get('host_ms_per_step',0),3))"
+             python3 -c "import json;a=json.load(open('$out/trainab$v.$r.json'));print('${AB_VAR:-AA_TRA_ROW}=$v train', round(a['value'],1), 'steps/s host ms', round(a.get('host_ms_per_step',0),3))"
            done; done ;;
     pipe) # pipelined-rate probe: depth 2/3/4 x slot streams raw/aux
            for ps in x; do for d in 2 3 4; do
@@ -48,7 +48,7 @@ for s in $steps; do
              python3 -c "import json;d=json.load(open('$out/pipe_${ps}_$d.json'));print('streams $ps depth $d seq', round(d['value']), 'pipe', round(d['pipelined']['value']))"
            done; done ;;
     bits) # bitwise A/B of env switches on one training step (each switch: value 1 vs 0), bf16 and fp32
-           for var in ${BITS_VARS:-AA_TRA_ROW AA_SPLITK_REDUCE}; do for dt in bf16 fp32; do
+           for var in ${BITS_VARS:-AA_TRA_ROW AB_ONE_STREAM}; do for dt in bf16 fp32; do
              for v in 1 0; do
                env $var=$v timeout -k 10 300 python tools/ab_bits.py dump /tmp/bits_${var}_${dt}_$v.npz --train $dt --batch 128 --T 18 > $out/bits_${var}_$v.log 2>&1; rc=$?
                echo "[bits $var $dt $v] exit $rc" >&3; [ $rc -eq 0 ] || exit $rc
