@@ -21,6 +21,8 @@ ABI_VERSION = 16
 DECODE_EXACT_VOCAB = 1
 DECODE_FP32_ENCODER = 2
 DECODE_ONE_STREAM = 512
+DECODE_SPLIT_RESCORE = 1024  # rescoring in its own launch per step (cross-check of the fused default)
+DECODE_RS_SELF = 2048  # test hook: fused launch's LSTM workgroups rescore unpublished rows themselves
 BEAM_FAST = 256
 TRAIN_BF16 = 128
 MAX_BEAM = 8

@@ -535,8 +535,9 @@ class Encoder2Decoder(nn.Module):
         return _lib.TRAIN_BF16 if getattr(self, "train_bf16", False) else 0
 
     def _decode_flags(self) -> int:
-        """Flags of a default greedy decode (what sampler passes without exact_vocab)."""
-        return _lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0
+        """Flags of a default greedy decode (what sampler passes without exact_vocab), plus
+        ``decode_extra_flags`` (e.g. ``_lib.DECODE_SPLIT_RESCORE``, the cross-check launch structure)."""
+        return (_lib.DECODE_FP32_ENCODER if self.fp32_encoder else 0) | int(getattr(self, "decode_extra_flags", 0))
 
     def _workspace(self, nbytes: int, dev) -> Optional[torch.Tensor]:
         if nbytes == 0:

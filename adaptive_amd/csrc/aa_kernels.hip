@@ -949,10 +949,11 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-template <int H, class F>
+template <int H, int NG = LS_GATHERS, class F>
 __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
                                               const bf16x8* wf1, bf16x8* stg, float* Pt, F&& pre) {
   constexpr int KC = H / 16, CP = LS_CP, N = KC / 2, NB = LS_NB < N ? LS_NB : N;
+  constexpr int LS_GATHERS = NG;  // ordinary loads `pre` issues (0: none)
   static_assert(NB >= 3, "the ring needs at least three stages");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
@@ -1036,7 +1037,33 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
 #ifndef AA_LSTM_OCC
 #define AA_LSTM_OCC 4
 #endif
-template <int H, bool G = false>
+// The previous step's rescoring, run inside k_lstm<H, false, true> (greedy steps t >= 1): workgroups
+// 0 .. NR-1 rescore rows 2 bid, 2 bid + 1 of step t - 1 (k_vrescore's body, two 256-thread groups)
+// and publish each row's argmax key as one agent-scope 8-byte store into keys[t-1] (zeroed before
+// the decode, so a nonzero key is the readiness tag); the GEMM workgroups run the token-independent
+// h W_hh^T phase meanwhile and only then wait for their 64 rows' keys.  A GEMM workgroup never waits
+// on a workgroup that might not be resident: past RS_WAIT_TICKS of polling it rescores the missing
+// rows itself (the same function on the same inputs: the same key), so the launch cannot deadlock
+// whatever the dispatch order or the co-resident work of other streams.
+struct RsArgs {
+  int NR, Vp, T, t_step;
+  uint64_t wait;  // poll bound in ticks of the 100 MHz clock (RS_WAIT_TICKS; 0: AA_DECODE_RS_SELF)
+  const float* u;
+  const float4* summ;
+  const float* W;
+  const float* bias;
+  uint64_t* keys;  // keys[t-1] (B entries)
+  int64_t* ids;
+};
+template <int H>
+struct RsScratch;
+template <int H, bool PUB>
+__device__ __forceinline__ uint64_t rescore_row(int b, bool write, int t, int V, int Vp, const float* __restrict__ u,
+                                                const float4* __restrict__ summ, const float* __restrict__ W,
+                                                const float* __restrict__ bias, uint64_t* __restrict__ keys,
+                                                int64_t* __restrict__ ids, int T, int t_step, float* scr);
+constexpr uint64_t RS_WAIT_TICKS = 5000;  // 50 us of the 100 MHz constant clock
+template <int H, bool G = false, bool RS = false>
 __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
@@ -1044,17 +1071,29 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
                                               const bf16x8* __restrict__ whh3,
                                               const float* __restrict__ wgs, float* __restrict__ h_out,
                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
-                                              float* __restrict__ s_out, float* __restrict__ part) {
+                                              float* __restrict__ s_out, float* __restrict__ part, RsArgs ra) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
   AA_TS(0, 0);
   // the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
   constexpr int RING_FLOATS = (LS_NB < H / 32 ? LS_NB : H / 32) * LS_STAGE * 4;
-  constexpr int LDS_FLOATS = RING_FLOATS + 64;  // + the tile's 64 tokens
+  constexpr int LDS_FLOATS = RING_FLOATS + 64 + 4;  // + the tile's 64 tokens (+ RS: the missing-row mask)
   static_assert(TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
-  const int L = xcd_remap(blockIdx.x, MT * NTn);
+  int bid = blockIdx.x;
+  if constexpr (RS) {
+    static_assert(!G, "the fused rescoring is the greedy path's");
+    static_assert(TS + 2 * RsScratch<H>::FLOATS <= RING_FLOATS, "two rescoring scratch areas beside the tile");
+    if (bid < ra.NR) {  // rescoring role (uniform per workgroup): rows 2 bid + (t >> 8)
+      const int row = 2 * bid + (int)(threadIdx.x >> 8);
+      rescore_row<H, true>(row < B ? row : B - 1, row < B, threadIdx.x & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
+                           ra.bias, ra.keys, ra.ids, ra.T, ra.t_step, lds + (threadIdx.x >> 8) * RsScratch<H>::FLOATS);
+      return;
+    }
+    bid -= ra.NR;
+  }
+  const int L = xcd_remap(bid, MT * NTn);
   const int nt = L / MT, mt = L % MT;  // m fastest: a weight tile is shared inside an XCD
   const int t = threadIdx.x, lane = t & 63;
   const int m0 = mt * BM;
@@ -1115,14 +1154,52 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
   // the token-dependent gathers (exactly LS_GATHERS loads, counted by the ring's waits)
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
-    // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
-    if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    tk = tok ? tok_lds[rr] : 1;
+  if constexpr (RS) {
+    // the GEMM phase alone (no token yet), then the keys of the tile's rows, then the gathers
+    lstm_gemm_lds<H, 0>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [] {});
+    __syncthreads();
+    uint64_t* miss = reinterpret_cast<uint64_t*>(lds + RING_FLOATS + 64);
+    if (t < 64) {
+      const int r = m0 + t < B ? m0 + t : B - 1;
+      uint64_t k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = wall_clock64();
+      while (!__all(k != 0)) {  // wave-uniform: bounded poll of the 8-byte granules
+        if (wall_clock64() - t0 > ra.wait) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (k == 0) k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      tok_lds[t] = (int)key_token(k);
+      const uint64_t mb = __ballot(k == 0);
+      if (t == 0) *miss = mb;
+    }
+    __syncthreads();
+    uint64_t mb = *miss;
+    // rows not yet published: rescored here, two at a time (the tile's Pt stays below the scratch)
+    while (mb) {
+      const int i0 = __builtin_ctzll(mb);
+      mb &= mb - 1;
+      const int i1 = mb ? __builtin_ctzll(mb) : i0;
+      if (mb) mb &= mb - 1;
+      const int i = (t >> 8) ? i1 : i0;
+      const int r = m0 + i < B ? m0 + i : B - 1;
+      const uint64_t k = rescore_row<H, true>(r, (t >> 8) == 0 || i1 != i0, t & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
+                                              ra.bias, ra.keys, ra.ids, ra.T, ra.t_step,
+                                              lds + TS + (t >> 8) * RsScratch<H>::FLOATS);
+      if ((t & 255) == 0) tok_lds[i] = (int)key_token(k);
+      __syncthreads();
+    }
+    tk = tok_lds[rr];
     gathers();
-    asm volatile("" ::: "memory");
-  });
+  } else {
+    lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
+      // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
+      if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      tk = tok ? tok_lds[rr] : 1;
+      gathers();
+      asm volatile("" ::: "memory");
+    });
+  }
   AA_TS(0, 1);
   __syncthreads();
   float gate[4][2];
@@ -2094,18 +2171,30 @@ __device__ __forceinline__ float exact_logit8(const float* __restrict__ urow, co
 #define AA_RS_THREADS 256
 #endif
 constexpr int RS_NT = AA_RS_THREADS, RS_NW = RS_NT / 64;
+// LDS scratch of one rescored row (floats): u row, candidate list, count, wave maxima, wave keys
 template <int H>
-__global__ __launch_bounds__(RS_NT) void k_vrescore(int B, int V, int Vp, const float* __restrict__ u,
-                                                  const float4* __restrict__ summ, const float* __restrict__ W,
-                                                  const float* __restrict__ bias, uint64_t* __restrict__ keys,
-                                                  int64_t* __restrict__ ids, int T, int t_step) {
-  __shared__ __attribute__((aligned(16))) float urow[H];
-  __shared__ int cand[RS_CAP];
-  __shared__ int ncand;
-  __shared__ float wmax[RS_NW];
-  __shared__ uint64_t wbest[RS_NW];
-  AA_TS(3, 0);
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+struct RsScratch {
+  static constexpr int URow = 0, Cand = H, NCand = H + RS_CAP, WMax = NCand + 4, WBest = WMax + RS_NW + 4,
+                       FLOATS = WBest + 2 * RS_NW;
+  static_assert(H % 4 == 0 && WBest % 2 == 0, "16-B u row, 8-B keys");
+};
+// The rescoring of one row by RS_NT threads (t = 0 .. RS_NT-1 of the calling group; every thread of
+// the workgroup reaches the same three barriers): k_vrescore's body.  PUB: the key is stored by an
+// agent-scope atomic store (a write-through granule that k_lstm<.., RS> polls within its launch);
+// write = false computes without storing (a padding group that only keeps the barrier count).
+// Returns the row's key in every thread.
+template <int H, bool PUB>
+__device__ __forceinline__ uint64_t rescore_row(int b, bool write, int t, int V, int Vp, const float* __restrict__ u,
+                                                const float4* __restrict__ summ, const float* __restrict__ W,
+                                                const float* __restrict__ bias, uint64_t* __restrict__ keys,
+                                                int64_t* __restrict__ ids, int T, int t_step, float* scr) {
+  typedef RsScratch<H> S;
+  float* urow = scr + S::URow;
+  int* cand = reinterpret_cast<int*>(scr + S::Cand);
+  int& ncand = *reinterpret_cast<int*>(scr + S::NCand);
+  float* wmax = scr + S::WMax;
+  uint64_t* wbest = reinterpret_cast<uint64_t*>(scr + S::WBest);
+  const int lane = t & 63, w = t >> 6;
   const int NTn = Vp / VS_TILE;
   for (int d = 4 * t; d < H; d += 4 * RS_NT) *reinterpret_cast<float4*>(&urow[d]) = *reinterpret_cast<const float4*>(u + (int64_t)b * H + d);
   if (t == 0) ncand = 0;
@@ -2157,12 +2246,25 @@ __global__ __launch_bounds__(RS_NT) void k_vrescore(int B, int V, int Vp, const 
   best = wave_max_u64(best);
   if (lane == 0) wbest[w] = best;
   __syncthreads();
-  if (t == 0) {
-    uint64_t k = wbest[0];
-    for (int i = 1; i < RS_NW; ++i) k = wbest[i] > k ? wbest[i] : k;
-    keys[b] = k;
+  uint64_t k = wbest[0];
+#pragma unroll
+  for (int i = 1; i < RS_NW; ++i) k = wbest[i] > k ? wbest[i] : k;
+  if (t == 0 && write) {
     if (ids) ids[(int64_t)b * T + t_step] = key_token(k);
+    if constexpr (PUB) __hip_atomic_store(keys + b, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else keys[b] = k;
   }
+  return k;
+}
+
+template <int H>
+__global__ __launch_bounds__(RS_NT) void k_vrescore(int B, int V, int Vp, const float* __restrict__ u,
+                                                  const float4* __restrict__ summ, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, uint64_t* __restrict__ keys,
+                                                  int64_t* __restrict__ ids, int T, int t_step) {
+  __shared__ __attribute__((aligned(16))) float scr[RsScratch<H>::FLOATS];
+  AA_TS(3, 0);
+  rescore_row<H, false>(blockIdx.x, true, threadIdx.x, V, Vp, u, summ, W, bias, keys, ids, T, t_step, scr);
   AA_TS(3, 3);
 }
 
@@ -2688,18 +2790,26 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 
 // LSTM step (GEMM + cell in one launch), shared by the step API, the greedy loop and beam search.
 // par != nullptr: beam search (rows continue rows par[] of the previous step)
+// ra != nullptr: greedy step t >= 1 with step t-1's rescoring in the same launch (k_lstm<.., RS>); the
+// tokens come from the published keys, `tok` is not read
 static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
                         const bf16x8* hsp_in, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
-                        float* s_buf, float* part, hipStream_t s, const int* par = nullptr) {
+                        float* s_buf, float* part, hipStream_t s, const int* par = nullptr,
+                        const RsArgs* ra = nullptr) {
   const int H = L.H, MT = (B + 63) / 64;
+  const RsArgs none{};
 #define AA_LSTM(H_)                                                                                          \
   do {                                                                                                       \
     if (par)                                                                                                 \
       hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part); \
+                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none); \
+    else if (ra)                                                                                             \
+      hipLaunchKernelGGL((k_lstm<H_, false, true>), dim3(ra->NR + MT * (H_ / 16)), dim3(512), 0, s, B, L.V,    \
+                         nullptr, 0, p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, \
+                         part, *ra);                                                                         \
     else                                                                                                     \
       hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part);  \
+                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none); \
   } while (0)
   switch (H) {
     case 256: AA_LSTM(256); break;
@@ -2754,9 +2864,9 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
                               const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out, float* s_buf, float* part, float* u, uint16_t* ub,
                               float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
                               const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1,
-                              bf16x8* ub3 = nullptr) {
+                              bf16x8* ub3 = nullptr, const RsArgs* ra = nullptr) {
   rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
-  lstm_launch(L, p, B, tok, tok_ld, xg, hsp_in, c_in, h_out, hsp_out, c_out, s_buf, part, s, par);
+  lstm_launch(L, p, B, tok, tok_ld, xg, hsp_in, c_in, h_out, hsp_out, c_out, s_buf, part, s, par, ra);
   rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
   rec(tr ? tr->atten_events : nullptr, 2 * t, s);
   atten_launch(L, p, B, V, vwv, h_out, s_buf, part, u, ub, unorm, alpha, alpha_ld, beta, beta_ld, s, kdiv, ub3);
@@ -2814,6 +2924,9 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
   const int H = L.H, MT = (B + 63) / 64;
   const bool wide = screen_wide(L);
+  // the rescoring of step t-1 rides in step t's LSTM launch (k_lstm<.., RS>); the last step's has
+  // its own launch
+  const bool fused = !exact && (flags & AA_DECODE_SPLIT_RESCORE) == 0;
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
     // token of step t-1: ids[:, t-1] (written by the previous step); t = 0: nullptr = <start> for every row
@@ -2822,9 +2935,11 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
     uint64_t* kt = w.keys + (size_t)t * B;
     float* alt = alpha ? alpha + (size_t)t * P : nullptr;
     float* blt = beta ? beta + t : nullptr;
+    RsArgs ra{rup((B + 1) / 2, 8), L.Vp, T, t - 1, (flags & AA_DECODE_RS_SELF) ? 0 : RS_WAIT_TICKS, w.u, w.summ,
+              p.mlp_w, p.mlp_b, kt - B, ids};
     lstm_atten_launch(L, p, B, tok, tok_ld, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt], w.c[nxt],
                       w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm, alt, (int64_t)T * P, blt,
-                      T, trace, t, s, nullptr, 1, nullptr);
+                      T, trace, t, s, nullptr, 1, nullptr, fused && t > 0 ? &ra : nullptr);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     rec(sev, 2 * t, s);
@@ -2853,6 +2968,7 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
       default: AA_SCREEN(1024); break;
     }
     rec(sev, 2 * t + 1, s);
+    if (fused && t + 1 < T) continue;  // rescored by step t+1's k_lstm
     rec(rev, 2 * t, s);
     switch (H) {
       case 256: AA_RESCORE(256); break;
@@ -2884,16 +3000,17 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
-  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
-                      trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0]);
-  if (rc) return rc;
-  if (flags & AA_DECODE_EXACT_VOCAB) {
-    // the exact vocab stage accumulates into keys by atomicMax (k_vocab); the default stage writes
-    // every key it produces, so it needs no clearing (and step 0's k_lstm takes <start> itself)
+  if ((flags & AA_DECODE_EXACT_VOCAB) || ((flags & AA_DECODE_SPLIT_RESCORE) == 0 && T > 1)) {
+    // keys [T][B] cleared: the exact vocab stage accumulates into them by atomicMax (k_vocab); the
+    // fused rescoring publishes them as readiness-tagged granules (a nonzero key = ready, k_lstm<.., RS>).
+    // (The split default writes every key it produces; step 0's k_lstm takes <start> itself.)
     const int n = T * B, nblk = n / 256 + 1;
     hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1, w.keys,
                        n);
   }
+  rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
+                      trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0]);
+  if (rc) return rc;
   return decode_rows(L, p, w, B, T, flags, ids, alpha, beta, trace, s);
 }
 

@@ -122,7 +122,9 @@ typedef struct aa_model {
  *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
  *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen2 /
  *                   k_vscreen (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused
- *                   under AA_DECODE_EXACT_VOCAB); lstm = k_lstm;
+ *                   under AA_DECODE_EXACT_VOCAB; by default only pair T-1 is recorded: the rescoring
+ *                   of steps 0..T-2 runs inside the next step's LSTM launch); lstm = k_lstm (steps
+ *                   >= 1 by default include the previous step's rescoring);
  *   gemm_events:    unused (kept for layout stability; may be NULL). */
 #define AA_TRACE_ENCODER_KERNELS 5
 typedef struct aa_trace {
@@ -180,6 +182,11 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
                                     the default fp32-accurate 3-way-split bf16 MFMA (k_enc_v4) */
 #define AA_DECODE_ONE_STREAM 512 /* decode plans: capture the whole decode on one stream (no side-stream
                                      branch for the encoder's a_g work); for several plans in flight */
+#define AA_DECODE_SPLIT_RESCORE 1024 /* rescore each step in its own launch (k_vrescore) instead of inside
+                                        the next step's LSTM launch; the same ids (cross-check path) */
+#define AA_DECODE_RS_SELF 2048 /* test hook: the LSTM workgroups do not wait for the rescoring workgroups
+                                  of their launch but rescore every row not yet published themselves
+                                  (the fallback that keeps the fused launch deadlock-free); same ids */
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];

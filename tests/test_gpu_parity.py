@@ -299,6 +299,26 @@ def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device)
     assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
 
 
+@pytest.mark.parametrize("B,T", [(512, 20), (300, 9), (67, 5), (1, 4), (3, 2), (130, 1)])
+def test_fused_rescoring_equals_split(B, T, gpu_device):
+    """Step t-1's rescoring inside step t's LSTM launch (the default) == its own launch per step
+    (AA_DECODE_SPLIT_RESCORE) == the LSTM workgroups rescoring every unpublished row themselves
+    (AA_DECODE_RS_SELF, the no-wait fallback that keeps the fused launch deadlock-free): ids, alpha
+    and beta bit for bit, on odd and single-row batches and T = 1 (no fused launch)."""
+    from adaptive_amd import _lib
+    m = _model(99, 0.02)
+    feats = torch.from_numpy(synth.make_features(B, seed=B + T)).to(gpu_device)
+    a = m.sampler(feats, max_len=T)
+    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF):
+        m.decode_extra_flags = extra
+        b = m.sampler(feats, max_len=T)
+        m.decode_extra_flags = 0
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), extra
+    ex = m.sampler(feats, max_len=T, exact_vocab=True)
+    assert torch.equal(ex[0], a[0])
+
+
 def test_all_columns_tied_rescore_overflow(gpu_device):
     """W_m = 0, b_m = 0: every logit is exactly 0, so every column is a candidate (k_vrescore's
     candidate list overflows into its all-columns fallback).  The first index (0) must win
