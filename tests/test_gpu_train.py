@@ -218,6 +218,33 @@ def test_train_bf16_vs_oracle(gpu_device):
     assert not torch.equal(p32[0].detach(), packed[0].detach())
 
 
+def test_train_bf16_small_vocab_vs_fp32(gpu_device):
+    """A vocabulary far below the channel count (100 < 2048) at a small batch: the bf16 step's packed
+    W_a slot is sized for the larger of the two (the slot held only H x rup64(vocab)), so
+    the encoder GEMM's operands are intact -- the bf16 step agrees with the fp32 step within the bf16
+    tolerances, gradients included."""
+    B, L = 4, 7
+    lengths = [6, 5, 5, 3]
+    cf = Config(vocab_length=100)
+    rng = np.random.default_rng(2)
+    caps = torch.from_numpy(rng.integers(0, 100, size=(B, L)).astype(np.int64)).to(gpu_device)
+    caps[:, 0] = 1
+    feats = torch.from_numpy(synth.make_features(B, seed=4)).to(gpu_device)
+    out = {}
+    for bf16 in (False, True):
+        model = Encoder2Decoder(cf).to(gpu_device).load_synthetic(5, bias_noise=0.01)
+        model.train_bf16 = bf16
+        loss, packed = _loss(model, feats, caps, lengths)
+        loss.backward()
+        out[bf16] = (packed[0].detach().double(), loss.item(), {k: p.grad.detach().double() for k, p in model.named_parameters()})
+    s32, l32, g32 = out[False]
+    s16, l16, g16 = out[True]
+    assert torch.linalg.norm(s16 - s32) <= BF16_SCORE_REL * torch.linalg.norm(s32)
+    assert abs(l16 - l32) <= BF16_LOSS_REL * abs(l32)
+    for k in g32:
+        assert torch.linalg.norm(g16[k] - g32[k]) <= BF16_GRAD_REL * max(torch.linalg.norm(g32[k]).item(), 1e-30), k
+
+
 def test_train_bf16_deterministic_and_reduces_loss(gpu_device):
     B, L = 8, 10
     lengths = [9, 8, 8, 6, 5, 5, 3, 2]
