@@ -533,6 +533,10 @@ def main():
                     "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"],
                     "duration_source": f"HIP events ({timing_flags_used()}) on the launch stream around each "
                                        f"launch, traced region"}
+        if dominant == "k_lstm":
+            roofline["note"] = ("steps 1..T-1: one launch runs h W_hh^T + the cell (the FLOPs priced here) AND the "
+                                "exact rescoring of the previous step's vocabulary candidates (not priced); "
+                                "k_lstm averages the step-0 launch (no rescoring) in")
     # k_atten's per-step re-read of V, priced on its own whichever kernel is dominant (k_lstm and
     # k_atten are within a few per cent of each other)
     atten_v = None
@@ -585,7 +589,8 @@ def main():
                    + ("" if backend == "nccl" else f" ({backend} rehearsal)"),
                    "batches_in_flight": 1, "feature_buffers": nbuf,
                    "launch": "direct kernel launches from one C call per sampler() (no hipGraph, no per-buffer cache)",
-                   "vocab_stage": "k_vscreen2 (bf16 screen, granule summaries) + k_vrescore (exact fp32 rescoring)",
+                   "vocab_stage": "k_vscreen2 (bf16 screen, granule summaries) + exact fp32 rescoring of the "
+                                  "candidates inside the next step's k_lstm launch (k_vrescore for the last step)",
                    "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy",
                    "headline": "one sampler() call after another on resident batches"},
         "ranks_seen": dist.get_world_size() if world > 1 else 1,
