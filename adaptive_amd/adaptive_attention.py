@@ -274,7 +274,9 @@ class Encoder2Decoder(nn.Module):
         # None = as the reference (every visible device when there is more than one, unless a
         # multi-rank process group is initialised); False = this device only; True = every visible
         # device; or a list of device indices (the first should be the images' device).
-        self.device_parallel = None
+        # single-process multi-device sampler (device_parallel.py): opt-in -- True (every visible
+        # device) or a device list; False / None keep the decode on the images' device
+        self.device_parallel = False
         self._replicas = {}  # device index -> device_parallel._Replica
 
     # ---- weights -------------------------------------------------------------------------------
@@ -382,10 +384,11 @@ class Encoder2Decoder(nn.Module):
         so a fresh batch per call (code_src/tools/utils.py:167-171) costs what a resident one does.
         For repeated decodes of one shape, ``DecodePlan`` replays a captured hipGraph over its own
         buffers.
-        Several GPUs in this process (``device_parallel``, default as the reference's
-        ``torch.cuda.device_count() > 1`` test, adaptive_attention.py:178-181): the rows are split
-        into contiguous blocks, one per device, decoded concurrently (device_parallel.py) and
-        gathered onto the images' device -- the same values as one decode of all rows.
+        Several GPUs in this process (``self.device_parallel = True`` or a device list; opt-in, the
+        counterpart of the reference's ``torch.cuda.device_count() > 1`` test,
+        adaptive_attention.py:178-181): the rows are split into contiguous blocks, one per device,
+        decoded concurrently (device_parallel.py) and gathered onto the images' device -- the same
+        values as one decode of all rows.
         With ``self.distributed_sampler = True`` and an initialised multi-rank process group, every
         rank passes the whole batch and the call runs ``sharded_sampler`` (one process per GPU)."""
         if trace is None:
@@ -402,12 +405,8 @@ class Encoder2Decoder(nn.Module):
     def _parallel_devices(self, images: torch.Tensor, multi_rank: bool):
         """Device indices for a single-process multi-device decode, or None (this device only)."""
         mode = self.device_parallel
-        if mode is False or not images.is_cuda:
+        if mode is False or mode is None or not images.is_cuda:  # opt-in (see __init__)
             return None
-        if mode is None:  # as the reference: every visible device when there are several
-            if multi_rank or torch.cuda.device_count() < 2:
-                return None
-            mode = True
         home = images.device.index if images.device.index is not None else torch.cuda.current_device()
         if mode is True:
             devs = [home] + [d for d in range(torch.cuda.device_count()) if d != home]

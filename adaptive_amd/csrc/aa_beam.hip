@@ -662,8 +662,8 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
     lstm_atten_launch(L, p, R, t ? w.tok : w.tok0, 1, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt],
                       w.c[nxt], w.s, w.part, w.u, nullptr, nullptr, w.ahist + (size_t)t * R * P, P,
                       w.bhist + (size_t)t * R, 1, nullptr, t, s, t ? w.par : nullptr, K, exact ? nullptr : w.u3);
-    rec(vocab_events, 2 * t, s);
     if (exact) {
+      if (flags & AA_DECODE_EXACT_VOCAB) rec(vocab_events, 2 * t, s);
       // exact fp32 logits (k_vocab's fma chains, pitch Vp) and their granule summaries: one fused
       // launch (k_vexact), or -- AA_DECODE_EXACT_VOCAB, the cross-check -- k_vocab then k_gsumm
       if (flags & AA_DECODE_EXACT_VOCAB) {
@@ -672,20 +672,20 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
         hipLaunchKernelGGL(k_gsumm, dim3((unsigned)((((R + 31) / 32) * (L.Vp / 32) + 3) / 4)), dim3(256), 0, s, R,
                            L.V, L.Vp, w.logits, w.gsum);
       } else {
-        hipLaunchKernelGGL(k_vexact, dim3(((R + VX_BM - 1) / VX_BM) * (L.Vp / VX_BN)), dim3(256), 0, s, R, H, L.V,
-                           L.Vp, w.u, p.mlp_w, p.mlp_b, w.logits, w.gsum);
+        AA_TLAUNCH(vocab_events, 2 * t, k_vexact, dim3(((R + VX_BM - 1) / VX_BM) * (L.Vp / VX_BN)), dim3(256), 0, s,
+                   R, H, L.V, L.Vp, (const float*)w.u, p.mlp_w, p.mlp_b, w.logits, w.gsum);
       }
-      rec(vocab_events, 2 * t + 1, s);
+      if (flags & AA_DECODE_EXACT_VOCAB) rec(vocab_events, 2 * t + 1, s);
       hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
                          w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     } else {
 #define AA_VB3(H_)                                                                                            \
   if (wide)                                                                                                   \
-    hipLaunchKernelGGL(k_vbeam5<H_>, dim3(((R + 255) / 256) * (L.Vp / 256)), dim3(1024), 0, s, R, L.V, L.Vp,     \
-                       w.u3, p.mlp_w3, p.mlp_b, w.logits, w.gsum);                                            \
+    AA_TLAUNCH(vocab_events, 2 * t, k_vbeam5<H_>, dim3(((R + 255) / 256) * (L.Vp / 256)), dim3(1024), 0, s, R, L.V, \
+               L.Vp, (const bf16x8*)w.u3, p.mlp_w3, p.mlp_b, w.logits, w.gsum);                                 \
   else                                                                                                        \
-    hipLaunchKernelGGL(k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, L.Vp, w.u3, \
-                       p.mlp_w3, p.mlp_b, w.logits, w.gsum)
+    AA_TLAUNCH(vocab_events, 2 * t, k_vbeam4<H_>, dim3(((R + 127) / 128) * (L.Vp / 128)), dim3(256), 0, s, R, L.V, \
+               L.Vp, (const bf16x8*)w.u3, p.mlp_w3, p.mlp_b, w.logits, w.gsum)
       // 256 x 256 tiles when the padded vocabulary is whole 256-column tiles (V = 10,123: 40 of them)
       const bool wide = L.Vp % 256 == 0;  // else 128 x 128 tiles (k_vbeam4)
       switch (H) {
@@ -695,7 +695,6 @@ int aa_beam_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, 
         default: AA_VB3(1024); break;
       }
 #undef AA_VB3
-      rec(vocab_events, 2 * t + 1, s);
       hipLaunchKernelGGL(k_beam_select3, dim3(B), dim3(64 * K), 0, s, K, L.V, L.Vp, R, t, end_id < 0 ? -1 : end_id,
                          w.logits, w.gsum, w.cum, w.fin, w.tok, w.par, w.htok, w.hpar);
     }

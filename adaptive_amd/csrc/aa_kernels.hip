@@ -23,6 +23,7 @@
 //                     adaptive_attention.py:132, 201
 //   exact-vocab path (scores output / verification): k_vocab (fp32 MFMA GEMM + fused argmax) + k_finalize
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -2228,10 +2229,12 @@ __device__ __forceinline__ uint64_t rescore_row(int b, bool write, int t, int V,
   for (int i = t + 2 * RS_NT; i < NTn; i += RS_NT) select(sm[i], i);
   __syncthreads();
   AA_TS(3, 2);
-  const bool all = ncand > RS_CAP;
+  // an empty list (summaries that are all NaN) or an overflowing one: every column; the key starts at
+  // the lowest non-zero key, so a published key is never 0 (0 = "not yet published" for k_lstm<.., RS>)
+  const bool all = ncand > RS_CAP || ncand == 0;
   const int n = all ? V : ncand;
   const int g = t >> 3, lane8 = t & 7;
-  uint64_t best = 0;
+  uint64_t best = argmax_key(-INFINITY, V - 1);
   for (int i = g; i < n; i += RS_NT / 8) {
     int col = all ? i : cand[i];
     const bool ok = col < V;
@@ -2579,6 +2582,19 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
 static inline void rec(aa_event_t* arr, int i, hipStream_t s) {
   if (arr) (void)hipEventRecord((hipEvent_t)arr[i], s);
 }
+// Per-kernel timing hook (aa_trace): with an event array, the pair (I, I + 1) is handed to the launch
+// itself (hipExtLaunchKernel's start / stop events), which stamps it with the dispatch's own begin /
+// end timestamps -- the figures rocprofv3's kernel trace reads -- and no event packet sits between the
+// timed launches.  (Round 4 recorded events around each launch: ~1.5-3 us per launch of skew, and a
+// traced decode 1.46x slower than an untraced one.)  Kernel names with commas go in parentheses.
+#define AA_TLAUNCH(EV, I, K, G, BL, SH, S, ...)                                                              \
+  do {                                                                                                       \
+    aa_event_t* ev_ = (EV);                                                                                  \
+    if (ev_)                                                                                                 \
+      hipExtLaunchKernelGGL(K, G, BL, SH, S, (hipEvent_t)ev_[(I)], (hipEvent_t)ev_[(I) + 1], 0u, __VA_ARGS__); \
+    else                                                                                                     \
+      hipLaunchKernelGGL(K, G, BL, SH, S, __VA_ARGS__);                                                      \
+  } while (0)
 
 // Encoder tail.  With an aux stream, the a_g branch (k_avgpool -> k_enc_heads -> x_g GEMM: HBM- and
 // latency-bound) runs beside the V branch (k_enc_v3 -> VWv GEMM: MFMA-bound); both read only the
@@ -2609,43 +2625,40 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     sa = aux;
   }
   auto heads_xg = [&](hipStream_t st) {
-    rec(ev, 4, st);
     const int NH = E + 2 * H;
     if (flags & AA_DECODE_FP32_ENCODER || C % 256) {
       const int MT = (B + 63) / 64, NTn = L.NHp / 64;
-      hipLaunchKernelGGL(k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
-                         v_g, h0, c0);
+      AA_TLAUNCH(ev, 4, k_enc_heads, dim3(MT * NTn), dim3(256), 0, st, a_g, B, C, E, H, L.NHp, p.heads_w, p.heads_b,
+                 v_g, h0, c0);
     } else if (NH % 80 == 0 && C % 512 == 0) {
-      hipLaunchKernelGGL((k_gemm3<5, 8, MODE_HEADS>), dim3(((B + 31) / 32) * (NH / 80)), dim3(512), 0, st, a_g, B, C,
-                         NH, p.heads_w4, p.heads_b, v_g, 0, h0, c0, E, H);
+      AA_TLAUNCH(ev, 4, (k_gemm3<5, 8, MODE_HEADS>), dim3(((B + 31) / 32) * (NH / 80)), dim3(512), 0, st,
+                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H);
     } else {
-      hipLaunchKernelGGL((k_gemm3<4, 4, MODE_HEADS>), dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st, a_g,
-                         B, C, NH, p.heads_w4, p.heads_b, v_g, 0, h0, c0, E, H);
+      AA_TLAUNCH(ev, 4, (k_gemm3<4, 4, MODE_HEADS>), dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st,
+                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H);
     }
-    rec(ev, 5, st);
     if (heads_done) (void)hipEventRecord(heads_done, st);
-    rec(ev, 8, st);
-    if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0)
-      hipLaunchKernelGGL((k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st, v_g, B, E,
-                         L.N5, p.wvg4, p.bias5, xg, L.N5, nullptr, nullptr, 0, 0);
-    else if (xg)
+    if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0) {
+      AA_TLAUNCH(ev, 8, (k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st,
+                 (const float*)v_g, B, E, L.N5, (const bf16x8*)p.wvg4, (const float*)p.bias5, xg, L.N5, (float*)nullptr,
+                 (float*)nullptr, 0, 0);
+    } else if (xg) {
+      rec(ev, 8, st);
       gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
-    rec(ev, 9, st);
+      rec(ev, 9, st);
+    }
   };
   const bool v4 = enc_v4(L, flags);
   if (v4) {
     // k_enc_v4 computes V and a_g in one pass over the feature map; the a_g branch (heads, x_g)
     // then runs on aux beside the VWv GEMM.  (Trace: the fused avg-pool is a zero-length pair.)
-    rec(ev, 0, s);
-    rec(ev, 1, s);
-    rec(ev, 2, s);
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
     if (H == 512)
-      hipLaunchKernelGGL((k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg),
-                         dim3(64 * AA_ENC4_NW), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
+      AA_TLAUNCH(ev, 2, (k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg), dim3(64 * AA_ENC4_NW), 0, s, feats, B, C,
+                 (const bf16x8*)p.enc_w4, (const float*)p.enc_a_b, V, a_g);
     else
-      hipLaunchKernelGGL(k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, p.enc_w4, p.enc_a_b, V, a_g);
-    rec(ev, 3, s);
+      AA_TLAUNCH(ev, 2, k_enc_v4<2>, dim3(nwg), dim3(512), 0, s, feats, B, C, (const bf16x8*)p.enc_w4,
+                 (const float*)p.enc_a_b, V, a_g);
     if (sa != s) {  // aux waits for a_g
       hipEvent_t agr = nullptr;
       AA_TRY(hipEventCreateWithFlags(&agr, hipEventDisableTiming));
@@ -2655,27 +2668,26 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     }
     heads_xg(sa);
   } else {
-    rec(ev, 0, sa);
-    hipLaunchKernelGGL(k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, sa, feats, nch, a_g);
-    rec(ev, 1, sa);
+    AA_TLAUNCH(ev, 0, k_avgpool, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, sa, feats, nch, a_g);
     heads_xg(sa);
-    rec(ev, 2, s);
     if (flags & AA_DECODE_FP32_ENCODER) {
       const int M = B * P, MT = (M + 63) / 64, NTn = H / 64;
-      hipLaunchKernelGGL(k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_a_w, p.enc_a_b, V);
+      AA_TLAUNCH(ev, 2, k_enc_v, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, (const float*)p.enc_a_w,
+                 (const float*)p.enc_a_b, V);
     } else {
       const int M = B * P, MT = (M + EV_BM - 1) / EV_BM, NTn = H / EV_BN;
-      hipLaunchKernelGGL(k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, p.enc_w3, p.enc_a_b, V);
+      AA_TLAUNCH(ev, 2, k_enc_v3, dim3(MT * NTn), dim3(256), 0, s, feats, B, C, H, (const bf16x8*)p.enc_w3,
+                 (const float*)p.enc_a_b, V);
     }
-    rec(ev, 3, s);
   }
-  rec(ev, 6, s);
-  if (VWv && gemm3_ok(flags, H))
-    hipLaunchKernelGGL((k_gemm3<4, 4, MODE_PLAIN>), dim3((B * P + 31) / 32), dim3(256), 0, s, V, B * P, H, PP, p.wv4,
-                       nullptr, VWv, PP, nullptr, nullptr, 0, 0);
-  else if (VWv)
+  if (VWv && gemm3_ok(flags, H)) {
+    AA_TLAUNCH(ev, 6, (k_gemm3<4, 4, MODE_PLAIN>), dim3((B * P + 31) / 32), dim3(256), 0, s, (const float*)V, B * P, H,
+               PP, (const bf16x8*)p.wv4, (const float*)nullptr, VWv, PP, (float*)nullptr, (float*)nullptr, 0, 0);
+  } else if (VWv) {
+    rec(ev, 6, s);
     gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
-  rec(ev, 7, s);
+    rec(ev, 7, s);
+  }
   if (hsp0) {
     if (heads_done) AA_TRY(hipStreamWaitEvent(s, heads_done, 0));
     hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (H / 8) + 255) / 256)), dim3(256), 0, s, h0, B, H,
@@ -2795,21 +2807,22 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
                         const bf16x8* hsp_in, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
                         float* s_buf, float* part, hipStream_t s, const int* par = nullptr,
-                        const RsArgs* ra = nullptr) {
+                        const RsArgs* ra = nullptr, aa_event_t* ev = nullptr, int ei = 0) {
   const int H = L.H, MT = (B + 63) / 64;
   const RsArgs none{};
+  const int64_t* tnull = nullptr;
 #define AA_LSTM(H_)                                                                                          \
   do {                                                                                                       \
     if (par)                                                                                                 \
-      hipLaunchKernelGGL((k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none); \
+      AA_TLAUNCH(ev, ei, (k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,     \
+                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none);    \
     else if (ra)                                                                                             \
-      hipLaunchKernelGGL((k_lstm<H_, false, true>), dim3(ra->NR + MT * (H_ / 16)), dim3(512), 0, s, B, L.V,    \
-                         nullptr, 0, p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, \
-                         part, *ra);                                                                         \
+      AA_TLAUNCH(ev, ei, (k_lstm<H_, false, true>), dim3(ra->NR + MT * (H_ / 16)), dim3(512), 0, s, B, L.V,   \
+                 tnull, 0, p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part,  \
+                 *ra);                                                                                       \
     else                                                                                                     \
-      hipLaunchKernelGGL((k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld, \
-                         p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none); \
+      AA_TLAUNCH(ev, ei, (k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,    \
+                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none);    \
   } while (0)
   switch (H) {
     case 256: AA_LSTM(256); break;
@@ -2827,17 +2840,19 @@ static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok,
 static void atten_launch(const Layout& L, const MP& p, int B, const float* V, const float* vwv, const float* h_out,
                          float* s_buf, float* part, float* u, uint16_t* ub, float* unorm, float* alpha,
                          int64_t alpha_ld, float* beta, int64_t beta_ld, hipStream_t s, int kdiv = 1,
-                         bf16x8* ub3 = nullptr) {
+                         bf16x8* ub3 = nullptr, aa_event_t* ev = nullptr, int ei = 0) {
   const int H = L.H;
+  const float* sb = s_buf;
+  const float* pt = part;
 #define AA_ATTEN(HPT_)                                                                                     \
-  hipLaunchKernelGGL(k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
-                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+  AA_TLAUNCH(ev, ei, k_atten<HPT_>, dim3(B), dim3(256), 0, s, B, H / 16, kdiv, h_out, sb, pt, V, vwv, p.wh, alpha, \
+             alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
 #define AA_ATTEN5(H_)                                                                                      \
-  hipLaunchKernelGGL(k_atten5<H_>, dim3(B), dim3(512), 0, s, B, kdiv, h_out, s_buf, part, V, vwv, p.wh, alpha, \
-                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+  AA_TLAUNCH(ev, ei, k_atten5<H_>, dim3(B), dim3(512), 0, s, B, kdiv, h_out, sb, pt, V, vwv, p.wh, alpha, \
+             alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
 #define AA_ATTEN5B(KB_)                                                                                    \
-  hipLaunchKernelGGL((k_atten5b<512, KB_>), dim3(B / KB_), dim3(512), 0, s, h_out, s_buf, part, V, vwv, p.wh, alpha, \
-                     alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
+  AA_TLAUNCH(ev, ei, (k_atten5b<512, KB_>), dim3(B / KB_), dim3(512), 0, s, h_out, sb, pt, V, vwv, p.wh, alpha, \
+             alpha_ld, beta, beta_ld, u, ub, unorm, ub3)
   if (H == 512 && kdiv >= 2 && kdiv <= 5 && B % kdiv == 0 && AA_ATTEN_BEAM) {  // beam: one workgroup per image
     switch (kdiv) {
       case 2: AA_ATTEN5B(2); break;
@@ -2865,12 +2880,10 @@ static void lstm_atten_launch(const Layout& L, const MP& p, int B, const int64_t
                               float* unorm, float* alpha, int64_t alpha_ld, float* beta, int64_t beta_ld,
                               const aa_trace* tr, int t, hipStream_t s, const int* par = nullptr, int kdiv = 1,
                               bf16x8* ub3 = nullptr, const RsArgs* ra = nullptr) {
-  rec(tr ? tr->lstm_events : nullptr, 2 * t, s);
-  lstm_launch(L, p, B, tok, tok_ld, xg, hsp_in, c_in, h_out, hsp_out, c_out, s_buf, part, s, par, ra);
-  rec(tr ? tr->lstm_events : nullptr, 2 * t + 1, s);
-  rec(tr ? tr->atten_events : nullptr, 2 * t, s);
-  atten_launch(L, p, B, V, vwv, h_out, s_buf, part, u, ub, unorm, alpha, alpha_ld, beta, beta_ld, s, kdiv, ub3);
-  rec(tr ? tr->atten_events : nullptr, 2 * t + 1, s);
+  lstm_launch(L, p, B, tok, tok_ld, xg, hsp_in, c_in, h_out, hsp_out, c_out, s_buf, part, s, par, ra,
+              tr ? tr->lstm_events : nullptr, 2 * t);
+  atten_launch(L, p, B, V, vwv, h_out, s_buf, part, u, ub, unorm, alpha, alpha_ld, beta, beta_ld, s, kdiv, ub3,
+               tr ? tr->atten_events : nullptr, 2 * t);
 }
 
 int aa_decode_step(const aa_model* m, int32_t B, const int64_t* tokens_in, const float* V, const float* VWv,
@@ -2942,41 +2955,36 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
                       T, trace, t, s, nullptr, 1, nullptr, fused && t > 0 ? &ra : nullptr);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
-    rec(sev, 2 * t, s);
     if (exact) {
-      hipLaunchKernelGGL(k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V, w.u, p.mlp_w,
-                         p.mlp_b, nullptr, kt);
-      rec(sev, 2 * t + 1, s);
+      AA_TLAUNCH(sev, 2 * t, k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V,
+                 (const float*)w.u, p.mlp_w, p.mlp_b, (float*)nullptr, kt);
       hipLaunchKernelGGL(k_key_ids, dim3((B + 255) / 256), dim3(256), 0, s, kt, B, ids + t, T);
       continue;
     }
 #define AA_SCREEN(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vscreen<H_>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V, L.Vp, \
-                     reinterpret_cast<const bf16x8*>(w.ub), w.unorm, reinterpret_cast<const bf16x8*>(p.mlp_wb),  \
-                     p.mlp_gs, p.mlp_b, w.summ)
+  AA_TLAUNCH(sev, 2 * t, k_vscreen<H_>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V, \
+             L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                                  \
+             reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
 #define AA_SCREEN2(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vscreen2<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, B, L.V, \
-                     L.Vp, reinterpret_cast<const bf16x8*>(w.ub), w.unorm,                                          \
-                     reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
+  AA_TLAUNCH(sev, 2 * t, k_vscreen2<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, B, \
+             L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                             \
+             reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
 #define AA_RESCORE(H_)                                                                                          \
-  hipLaunchKernelGGL(k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, w.u, w.summ, p.mlp_w, p.mlp_b, kt, \
-                     ids, T, t)
+  AA_TLAUNCH(rev, 2 * t, k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, (const float*)w.u,           \
+             (const float4*)w.summ, p.mlp_w, p.mlp_b, kt, ids, T, t)
     switch (H) {
       case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
       case 512: if (wide) AA_SCREEN2(512); else AA_SCREEN(512); break;
       case 768: AA_SCREEN(768); break;
       default: AA_SCREEN(1024); break;
     }
-    rec(sev, 2 * t + 1, s);
     if (fused && t + 1 < T) continue;  // rescored by step t+1's k_lstm
-    rec(rev, 2 * t, s);
     switch (H) {
       case 256: AA_RESCORE(256); break;
       case 512: AA_RESCORE(512); break;
       case 768: AA_RESCORE(768); break;
       default: AA_RESCORE(1024); break;
     }
-    rec(rev, 2 * t + 1, s);
 #undef AA_SCREEN
 #undef AA_SCREEN2
 #undef AA_RESCORE

@@ -22,9 +22,16 @@ communication:
   op on it (and the caching allocator may reuse the caller's inputs only after the copies).
 
 Every kernel's per-row arithmetic is independent of the batch size, so the gathered ids, alpha and
-beta equal one decode of all rows bit for bit (``tests/test_gpu_device_parallel.py``; on a
-one-GPU box the same code path runs with the device listed twice).  The RCCL multi-process path
-(``adaptive_amd.distributed``) is unchanged.
+beta equal one decode of all rows bit for bit (``tests/test_gpu_device_parallel.py``).  Peer access
+between the home device and each remote device is enabled explicitly (``hipDeviceEnablePeerAccess``,
+idempotent) before the first peer copy.  The RCCL multi-process path (``adaptive_amd.distributed``)
+is unchanged.
+
+Opt-in (``model.device_parallel = True`` or a device list): this path has run only on a one-GPU
+box, with the device listed repeatedly and ``FORCE_REMOTE`` set so the extra blocks take the
+remote-device machinery (replica pack, ``_ReplicaView`` plans, stream-local copies) on the same
+device.  It has never touched a second physical device, so a plain ``sampler`` call stays on the
+images' device unless asked.
 """
 from __future__ import annotations
 
@@ -37,6 +44,10 @@ from . import _lib
 from .adaptive_attention import ATT, DecodePlan
 
 MAX_PLANS_PER_DEVICE = 2  # block shapes kept captured per device (LRU); eviction waits for that plan only
+# test hook: treat every block as remote (a weight replica packed on its device, a plan over the
+# replica's weights, copies in and out) even on the images' own device -- how a one-GPU box runs the
+# remote-device machinery (tests/test_gpu_device_parallel.py)
+FORCE_REMOTE = False
 
 
 def plan_shards(B: int, devices: Sequence[int]) -> List[Tuple[int, int, int]]:
@@ -64,7 +75,7 @@ class _Replica:
 
     def __init__(self, owner, device: int):
         self.device = torch.device("cuda", device)
-        self.home = owner._packed is not None and owner._packed.device == self.device
+        self.home = None  # set by refresh(): the owner's packed weights live on this device
         self.model = None
         self.params: Dict[str, torch.Tensor] = {}
         self.packed = None
@@ -74,13 +85,17 @@ class _Replica:
     def refresh(self, owner, stream) -> None:
         """(Re)pack on this device if the owner's weights changed since the last pack."""
         owner._model_struct()
-        if self._owner_key == owner._pack_key:
+        # recomputed every call: the model may have moved to another device since this replica was made
+        home = owner._packed.device == self.device and not FORCE_REMOTE
+        if self._owner_key == owner._pack_key and self.home == home:
             return
         for p in self.plans.values():
             p.close()
         self.plans.clear()
         self._owner_key = owner._pack_key
+        self.home = home
         if self.home:
+            self.params, self.packed, self.model = {}, None, None
             return
         lib = _lib.load()
         named = dict(owner.named_parameters())
@@ -142,7 +157,7 @@ def _replica(owner, device: int) -> _Replica:
 def parallel_sampler(owner, images: torch.Tensor, T: int, devices: Sequence[int], exact_vocab: bool = False):
     """``owner.sampler(images, T)`` with the rows split over ``devices`` (see the module docstring).
     Returns (ids, alpha, beta) on the images' device."""
-    from .hip_events import copy_async, role_stream
+    from .hip_events import copy_async, enable_peer_access, role_stream
     images = owner._check_images(owner.features(images))
     owner._model_struct()  # pack on the home device first (replicas copy the same parameters)
     B, home = images.size(0), images.device
@@ -161,6 +176,7 @@ def parallel_sampler(owner, images: torch.Tensor, T: int, devices: Sequence[int]
         if i == 0 and d == home.index:
             home_shards.append((lo, hi))  # decoded in place after the remote launches are queued
             continue
+        enable_peer_access(home.index, d)  # both directions, once per pair (no-op for d == home)
         s = role_stream(d, "device-parallel")
         rep = _replica(owner, d)
         with torch.cuda.device(d), torch.cuda.stream(s):

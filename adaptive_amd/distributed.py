@@ -55,6 +55,39 @@ def gather_rows(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
     return torch.cat([buf[r * width: r * width + counts[r]] for r in range(world)], dim=0)
 
 
+def pack_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, list]:
+    """Row-wise byte packing of several [n, ...] tensors into one [n, W] int32 tensor (each row: the
+    rows of ``tensors`` in order, reinterpreted as 32-bit words), so that ONE all-gather moves them
+    all.  Returns the packed tensor and the spec ``unpack_rows`` needs.  Every element size must be a
+    multiple of 4 bytes (int64 ids, fp32 alpha / beta)."""
+    if not tensors:
+        raise ValueError("pack_rows needs at least one tensor")
+    n = tensors[0].size(0)
+    cols, spec = [], []
+    for t in tensors:
+        if t.size(0) != n:
+            raise ValueError("pack_rows: every tensor needs the same number of rows")
+        if t.element_size() % 4:
+            raise ValueError(f"pack_rows: {t.dtype} is not a multiple of 32 bits")
+        flat = t.contiguous().view(n, -1)
+        words = flat.view(torch.int32) if flat.numel() else flat.new_empty((n, 0), dtype=torch.int32)
+        cols.append(words)
+        spec.append((t.dtype, tuple(t.shape[1:]), words.size(1)))
+    return torch.cat(cols, dim=1).contiguous(), spec
+
+
+def unpack_rows(packed: torch.Tensor, spec: list) -> List[torch.Tensor]:
+    """Inverse of ``pack_rows`` over any number of rows (e.g. the gathered [total, W] buffer):
+    bit-exact views of the original dtypes and shapes."""
+    out, c = [], 0
+    n = packed.size(0)
+    for dtype, shape, w in spec:
+        words = packed[:, c:c + w].contiguous()
+        out.append(words.view(dtype).view((n,) + shape))
+        c += w
+    return out
+
+
 def local_rows(images: torch.Tensor, group=None) -> torch.Tensor:
     """This rank's contiguous row block of a batch every rank holds in full."""
     lo, hi = shard_bounds(images.size(0), dist.get_world_size(group), dist.get_rank(group))
@@ -65,13 +98,16 @@ def sharded_sampler(decode: Callable[[torch.Tensor, int], Tuple[torch.Tensor, ..
                     total: int, max_len: int, group=None, gather_attention: bool = False):
     """Decode this rank's rows with ``decode(images, max_len) -> (ids, alpha, beta)`` and all-gather
     the ids (and optionally alpha/beta) to every rank.  ``images_local`` is the rank's
-    ``shard_bounds(total, world, rank)`` block of the ``total``-row batch."""
+    ``shard_bounds(total, world, rank)`` block of the ``total``-row batch.  With ``gather_attention``
+    the three outputs travel packed row by row in one int32 buffer (``pack_rows``): still ONE
+    all-gather per call."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     lo, hi = shard_bounds(total, world, rank)
     if images_local.size(0) != hi - lo:
         raise ValueError(f"rank {rank} was given {images_local.size(0)} rows, its shard of {total} is {hi - lo}")
     ids, alpha, beta = decode(images_local, max_len)
-    ids_all = gather_rows(ids, total, group)
     if not gather_attention:
-        return ids_all, None, None
-    return ids_all, gather_rows(alpha, total, group), gather_rows(beta, total, group)
+        return gather_rows(ids, total, group), None, None
+    packed, spec = pack_rows(ids, alpha, beta)
+    ids_all, alpha_all, beta_all = unpack_rows(gather_rows(packed, total, group), spec)
+    return ids_all, alpha_all, beta_all

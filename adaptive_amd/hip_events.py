@@ -167,6 +167,34 @@ def role_stream(device, role: str) -> "torch.cuda.ExternalStream":
 
 
 HIP_MEMCPY_DEFAULT = 4  # hipMemcpyDefault: direction from the pointers (unified addressing)
+HIP_ERROR_PEER_ACCESS_ALREADY_ENABLED = 704
+_peer_done = set()
+
+
+def enable_peer_access(a: int, b: int) -> None:
+    """Let devices ``a`` and ``b`` read and write each other's memory (hipDeviceEnablePeerAccess in
+    both directions; idempotent: "already enabled" counts as success).  Done explicitly before the
+    first peer copy of a single-process multi-device decode instead of relying on a side effect of
+    torch's cross-device ``.to()``.  Raises if the pair cannot access each other (no P2P path)."""
+    a, b = int(a), int(b)
+    if a == b or (a, b) in _peer_done:
+        return
+    h = hip()
+    h.hipDeviceCanAccessPeer.argtypes = [ctypes.POINTER(c_int), c_int, c_int]
+    h.hipDeviceCanAccessPeer.restype = c_int
+    h.hipDeviceEnablePeerAccess.argtypes = [c_int, ctypes.c_uint]
+    h.hipDeviceEnablePeerAccess.restype = c_int
+    for src, dst in ((a, b), (b, a)):
+        ok = c_int(0)
+        rc = h.hipDeviceCanAccessPeer(ctypes.byref(ok), src, dst)
+        if rc != 0 or not ok.value:
+            raise RuntimeError(f"device {src} cannot access device {dst} (hipDeviceCanAccessPeer rc={rc})")
+        with torch.cuda.device(src):
+            rc = h.hipDeviceEnablePeerAccess(dst, 0)
+        if rc not in (0, HIP_ERROR_PEER_ACCESS_ALREADY_ENABLED):
+            raise RuntimeError(f"hipDeviceEnablePeerAccess({src} -> {dst}) failed: {rc}")
+    _peer_done.add((a, b))
+    _peer_done.add((b, a))
 
 
 def copy_async(dst: "torch.Tensor", src: "torch.Tensor", stream) -> None:

@@ -59,7 +59,11 @@ class DecodePipeline:
     hold two: reusing the side stream keeps three slots on three distinct queues besides the caller's
     (measured, depth 3, one box: 549 K captions/s against 444 K with three fresh streams, one of which
     shared a queue).  Two pipelines alive on one device share those streams and therefore serialise
-    against each other (results stay correct; only their overlap is lost)."""
+    against each other (results stay correct; only their overlap is lost).  For the same reason a
+    ``sampler()`` call on the same device while pipeline batches are in flight queues its encoder side
+    branch behind slot 0's whole decode and its stream then waits for it: the two serialise.  Results
+    stay correct, but do not interleave ``sampler()`` with a live pipeline where overlap matters --
+    submit the batch to the pipeline instead."""
 
     def __init__(self, model, max_len: int = 20, depth: int = 2, raw_streams: bool = True, streams=None):
         if depth < 1:

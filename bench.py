@@ -95,12 +95,21 @@ def kernel_costs(B: int, T: int) -> dict:
         "k_gemm3(heads)": ("mfma_x3", f["k_enc_heads"] * B),
         "k_gemm3(VWv)": ("mfma_x3", f["vwv"] * B),
         "k_gemm3(x_g)": ("mfma_x3", f["xg"] * B),
+        "k_lstm(step0)": ("mfma_x3", f["k_lstm"] * B),
+        # steps 1..T-1: the same GEMM + cell, and the launch also rescores step t-1 (rescore_bytes)
         "k_lstm": ("mfma_x3", f["k_lstm"] * B),
         "k_atten": ("hbm", (atten_bytes_per_row() - v_restream_bytes_per_row()) * B),
         "k_vscreen": ("mfma_bf16", f["k_vscreen"] * B),
         # per row: 320 granule summaries + u + the winning W_m row + id/key out (candidate count varies)
-        "k_vrescore": ("hbm", B * ((V + 127) // 128 * 4 * 16 + 4 * H + 4 * H + 16)),
+        "k_vrescore": ("hbm", B * rescore_bytes_per_row()),
     }
+
+
+def rescore_bytes_per_row(Vp: int = 10240) -> int:
+    """Algorithmic bytes of the exact rescoring of one row (k_vrescore, or inside the next step's
+    k_lstm launch): the row's Vp/32 granule summaries (float4 each), u, the winning W_m row, the key
+    and the id out.  Columns rescored beyond the winner depend on the data and are not counted."""
+    return Vp // 32 * 16 + 4 * H + 4 * H + 8 + 8
 
 
 def v_restream_bytes_per_row() -> int:
@@ -482,25 +491,31 @@ def main():
     kernels = {}
     if traces:
         traced_ms = 1e3 * traced_elapsed / K
-        enc_names = ("k_avgpool", "k_enc_v4", "k_gemm3(heads)", "k_gemm3(VWv)", "k_gemm3(x_g)")
-        per = {k: [] for k in enc_names[1:] + ("k_lstm", "k_atten", "k_vscreen", "k_vrescore")}
+        # encoder event pairs (aa_trace.encoder_events): 0 k_avgpool (fused into k_enc_v4: never
+        # launched on this path), 1 the V GEMM, 2 heads, 3 VWv, 4 x_g
+        enc_pairs = {"k_enc_v4": 1, "k_gemm3(heads)": 2, "k_gemm3(VWv)": 3, "k_gemm3(x_g)": 4}
+        per = {k: [] for k in list(enc_pairs) + ["k_lstm(step0)", "k_lstm", "k_atten", "k_vscreen", "k_vrescore"]}
         for ev, _ in traces:
-            enc = ev["encoder"].pair_durations_ms()
-            for i, k in enumerate(enc_names):
-                if k in per:  # (k_avgpool is fused into k_enc_v4: its trace pair is empty)
-                    per[k].append(enc[i])
-            for k, name in zip(kern, ("k_lstm", "k_atten", "k_vscreen", "k_vrescore")):
-                # only the last step's rescoring has its own launch; steps 0..T-2 are rescored inside
-                # the next step's k_lstm launch (aa_greedy_decode's default)
-                per[name] += [ev[k].elapsed_ms(2 * T - 2, 2 * T - 1)] if k == "rescore" else ev[k].pair_durations_ms()
+            for k, i in enc_pairs.items():
+                per[k].append(ev["encoder"].elapsed_ms(2 * i, 2 * i + 1))
+            lstm = ev["lstm"].pair_durations_ms()
+            per["k_lstm(step0)"].append(lstm[0])  # step 0: no previous step to rescore
+            per["k_lstm"] += lstm[1:]             # steps 1..T-1: + the rescoring of step t-1
+            per["k_atten"] += ev["atten"].pair_durations_ms()
+            per["k_vscreen"] += ev["screen"].pair_durations_ms()
+            # only the last step's rescoring has its own launch
+            per["k_vrescore"].append(ev["rescore"].elapsed_ms(2 * T - 2, 2 * T - 1))
         costs = kernel_costs(B, T)
         for k, ds in per.items():
-            avg_ms = float(np.mean(ds))
+            if not ds:
+                continue
+            med_ms = float(np.median(ds))
             per_step = len(ds) / K
             bound, amount = costs[k]
-            entry = {"avg_ms": avg_ms, "launches": len(ds), "ms_per_step": avg_ms * per_step,
-                     "share_of_step": avg_ms * per_step / traced_ms}
-            sec = avg_ms * 1e-3
+            entry = {"median_ms": med_ms, "avg_ms": float(np.mean(ds)), "min_ms": float(np.min(ds)),
+                     "max_ms": float(np.max(ds)), "launches": len(ds), "ms_per_step": med_ms * per_step,
+                     "share_of_step": med_ms * per_step / ms_per_step}
+            sec = med_ms * 1e-3
             if bound == "hbm":
                 entry.update({"bound": "hbm", "achieved": amount / sec / 1e9, "peak": PEAK_HBM / 1e9,
                               "unit": "GB/s", "algorithmic_bytes_per_launch": amount})
@@ -513,9 +528,19 @@ def main():
                                      "(fp32-accurate); algorithmic fp32 FLOPs priced against bf16 peak / 6")
                 if bound == "mfma_bf16":
                     entry["note"] = ("2HV vocab contraction on bf16 MFMA under a rigorous error bound (exact fp32 "
-                                     "rescoring of the candidates in k_vrescore); priced against the dense bf16 peak")
+                                     "rescoring of the candidates in the next step's k_lstm launch); priced against "
+                                     "the dense bf16 peak")
             entry["frac"] = entry["achieved"] / entry["peak"]
+            if k == "k_lstm":
+                rb = rescore_bytes_per_row() * B
+                ideal = amount / (entry["peak"] * 1e12) + rb / PEAK_HBM
+                entry.update({"rescore_bytes_per_launch": rb, "ideal_us_incl_rescoring": ideal * 1e6,
+                              "frac_incl_rescoring": ideal / sec,
+                              "note": entry["note"] + "; the launch also rescores step t-1's vocabulary "
+                                      "candidates exactly (rescore_bytes_per_launch at HBM peak): "
+                                      "frac_incl_rescoring = (FLOPs / peak + bytes / 8 TB/s) / duration"})
             kernels[k] = entry
+        kernel_sum = sum(e["ms_per_step"] for e in kernels.values())
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
     roofline = None
     traffic_all = {}
@@ -530,13 +555,21 @@ def main():
         traffic = traffic_all.get(pmc_name, {}).get("hbm_bytes_per_launch")
         roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
-                    "avg_launch_ms": kd["avg_ms"], "launches_timed": kd["launches"],
-                    "duration_source": f"HIP events ({timing_flags_used()}) on the launch stream around each "
-                                       f"launch, traced region"}
+                    "median_launch_ms": kd["median_ms"], "avg_launch_ms": kd["avg_ms"],
+                    "launches_timed": kd["launches"],
+                    "duration_source": "median over the traced region's launches of the dispatch's own start / end "
+                                       "timestamps (hipExtLaunchKernel start / stop events on the launch stream: "
+                                       "the timestamps rocprofv3's kernel trace reads; no event packet between "
+                                       "the launches); rocprofv3 summary of the same region: profiles/"}
+        for key in ("algorithmic_flops_per_launch", "algorithmic_bytes_per_launch", "rescore_bytes_per_launch",
+                    "ideal_us_incl_rescoring", "frac_incl_rescoring"):
+            if key in kd:
+                roofline[key] = kd[key]
         if dominant == "k_lstm":
-            roofline["note"] = ("steps 1..T-1: one launch runs h W_hh^T + the cell (the FLOPs priced here) AND the "
-                                "exact rescoring of the previous step's vocabulary candidates (not priced); "
-                                "k_lstm averages the step-0 launch (no rescoring) in")
+            roofline["note"] = ("steps 1..T-1: one launch runs h W_hh^T + the cell + the attention projections (the "
+                                "FLOPs priced in `frac`) AND the exact rescoring of the previous step's vocabulary "
+                                "candidates (priced in `frac_incl_rescoring` at HBM peak); the step-0 launch "
+                                "(no rescoring) is reported apart as k_lstm(step0)")
     # k_atten's per-step re-read of V, priced on its own whichever kernel is dominant (k_lstm and
     # k_atten are within a few per cent of each other)
     atten_v = None
@@ -544,14 +577,14 @@ def main():
         ka = kernels["k_atten"]
         vb = v_restream_bytes_per_row() * B
         mall = read_probe(dev, vb)
-        sec = ka["avg_ms"] * 1e-3
+        sec = ka["median_ms"] * 1e-3
         atten_v = {
             "bytes_per_launch": vb, "achieved_gbs": vb / sec / 1e9,
             "mall_read_ceiling_gbs": mall, "frac_of_mall_ceiling": vb / sec / 1e9 / mall,
             "algorithmic_bytes_per_launch": ka["algorithmic_bytes_per_launch"],
             "executed_bytes_per_launch": ka["algorithmic_bytes_per_launch"] + vb,
             "executed_achieved_gbs": (ka["algorithmic_bytes_per_launch"] + vb) / sec / 1e9,
-            "avg_launch_ms": ka["avg_ms"],
+            "median_launch_ms": ka["median_ms"],
             "note": "k_atten's per-step re-read of V (not algorithmic bytes, SURVEY.md §8d; 51.4 MB at B=512, "
                     "MALL-resident), priced against the MALL-served read rate of a V-sized buffer "
                     "measured here (aa_read_probe, re-read back to back)"}
@@ -635,6 +668,10 @@ def main():
                                   "figures"},
         "kernels": kernels,
         "traced_ms_per_step": None if traced_elapsed is None else 1e3 * traced_elapsed / K,
+        "kernel_sum_ms_per_step": kernel_sum if kernels else None,
+        "kernel_sum_note": "sum over the kernels of median duration x launches per step (the encoder's heads / x_g "
+                           "run on the aux stream beside the VWv GEMM, so they may overlap) against ms_per_step; "
+                           "the rest is launch boundaries and the ids copy",
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

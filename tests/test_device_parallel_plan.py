@@ -43,10 +43,11 @@ class _FakeImages:
 
 
 @pytest.mark.parametrize("mode,count,multi_rank,want", [
-    (None, 1, False, None),                 # one visible device: the plain decode (reference: no DataParallel)
-    (None, 8, False, [2, 0, 1, 3, 4, 5, 6, 7]),  # several: every device, the images' own first
-    (None, 8, True, None),                  # one process per GPU (torch.distributed): never fan out
+    (None, 1, False, None),                 # opt-in: off by default
+    (None, 8, False, None),
     (False, 8, False, None),
+    (True, 8, False, [2, 0, 1, 3, 4, 5, 6, 7]),  # every visible device, the images' own first
+    (True, 3, False, [2, 0, 1]),
     (True, 2, True, [2, 0, 1]),             # explicit: all visible devices even under a process group
     ([2, 5], 8, False, [2, 5]),
     ([2], 8, False, None),

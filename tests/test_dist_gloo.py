@@ -11,7 +11,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from adaptive_amd import synth
-from adaptive_amd.distributed import gather_rows, shard_bounds, sharded_sampler
+from adaptive_amd import distributed as D
+from adaptive_amd.distributed import gather_rows, pack_rows, shard_bounds, sharded_sampler, unpack_rows
 
 
 def _free_port():
@@ -28,6 +29,31 @@ def test_shard_bounds():
         shard_bounds(4, 2, 2)
 
 
+def test_pack_rows_layout_and_round_trip():
+    """The packed all-gather buffer: row r holds row r's int64 ids (two int32 words each), then its
+    alpha, then its beta, as raw 32-bit words; unpacking any row range gives the tensors back bit for
+    bit (NaN payloads and -0.0 included)."""
+    n, T = 3, 4
+    ids = torch.arange(n * T, dtype=torch.int64).view(n, T) * (1 << 33) + 7
+    alpha = torch.randn(n, T, 49)
+    alpha[1, 2, 3] = float("nan")
+    alpha[2, 0, 0] = -0.0
+    beta = torch.rand(n, T, 1)
+    packed, spec = pack_rows(ids, alpha, beta)
+    assert packed.dtype == torch.int32 and packed.shape == (n, 2 * T + 49 * T + T)
+    for r in range(n):
+        assert torch.equal(packed[r, :2 * T], ids[r].view(torch.int32))
+        assert torch.equal(packed[r, 2 * T:2 * T + 49 * T], alpha[r].reshape(-1).view(torch.int32))
+        assert torch.equal(packed[r, 2 * T + 49 * T:], beta[r].reshape(-1).view(torch.int32))
+    both = torch.cat([packed, packed[:2]])  # e.g. a gathered buffer of 5 rows
+    i2, a2, b2 = unpack_rows(both, spec)
+    assert i2.shape == (5, T) and a2.shape == (5, T, 49) and b2.shape == (5, T, 1)
+    assert torch.equal(i2[:n], ids) and torch.equal(b2[:n], beta)
+    assert torch.equal(a2[:n].view(torch.int32), alpha.view(torch.int32))
+    with pytest.raises(ValueError):
+        pack_rows(torch.zeros(2, 3, dtype=torch.int16))
+
+
 def _worker(rank, world, port, total, T, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -38,8 +64,15 @@ def _worker(rank, world, port, total, T, q):
         m = OracleModel(synth.make_weights(123))
         lo, hi = shard_bounds(total, world, rank)
         feats = torch.from_numpy(synth.make_features(hi - lo, seed=0, row0=lo))  # each rank makes only its rows
-        ids, alpha, beta = sharded_sampler(lambda x, t: m.sampler(x, max_len=t), feats, total, T,
-                                           gather_attention=True)
+        calls = []
+        real = D._all_gather
+        D._all_gather = lambda out, inp, group: (calls.append(tuple(inp.shape)), real(out, inp, group))
+        try:
+            ids, alpha, beta = sharded_sampler(lambda x, t: m.sampler(x, max_len=t), feats, total, T,
+                                               gather_attention=True)
+        finally:
+            D._all_gather = real
+        assert len(calls) == 1, calls  # ids, alpha and beta in ONE collective
         x = gather_rows(torch.arange(lo, hi, dtype=torch.int64).view(-1, 1), total)
         if rank == 0:
             q.put((ids, alpha, beta, x))

@@ -319,6 +319,26 @@ def test_fused_rescoring_equals_split(B, T, gpu_device):
     assert torch.equal(ex[0], a[0])
 
 
+def test_fused_rescoring_nan_vocab_weights(gpu_device):
+    """An all-NaN vocabulary projection leaves the screen's summaries NaN and the candidate lists
+    empty: the rescoring then scores every column and still publishes a non-zero key, so the fused
+    launch's GEMM workgroups find every key published (no 50 us bounded poll per step) and the three
+    launch structures agree bit for bit."""
+    from adaptive_amd import _lib
+    m = _model(5, 0.02)
+    with torch.no_grad():
+        m.decoder.adaptive.mlp.weight.fill_(float("nan"))
+    feats = torch.from_numpy(synth.make_features(67, seed=8)).to(gpu_device)
+    a = m.sampler(feats, max_len=4)
+    assert bool(((a[0] >= 0) & (a[0] < m.dims.vocab)).all())
+    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF):
+        m.decode_extra_flags = extra
+        b = m.sampler(feats, max_len=4)
+        m.decode_extra_flags = 0
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), extra
+
+
 def test_all_columns_tied_rescore_overflow(gpu_device):
     """W_m = 0, b_m = 0: every logit is exactly 0, so every column is a candidate (k_vrescore's
     candidate list overflows into its all-columns fallback).  The first index (0) must win
