@@ -36,20 +36,34 @@ namespace aa {
 constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
 
 // Vocab-screen error bound.  For one logit, the fp32 path (k_vocab / k_vrescore) computes
-// L = fl(sum_k u_k w_k) + b and the screen computes A = fl(sum_k bf16(u_k) bf16(w_k)) + b.
-// bf16 round-to-nearest has unit roundoff 2^-8, so |bf16(u)bf16(w) - uw| <= (2^-7 + 2^-16)|uw|;
-// both fp32 accumulations add <= gamma_H * sum|uw| each (gamma_512 ~ 3.1e-5).  Hence
-// |A - L| <= (0.0078125 + 1.6e-5 + 6.2e-5 (+ bias roundings)) * sum_k |u_k w_k|
-//         <= 0.00791 * ||u||_2 ||w||_2   (Cauchy-Schwarz).
-// The screen applies one bound per (row, 32-column granule g):
-//   E = CEPS ||u|| W_g + EPS_ABS (||u|| W_g + B_g),   W_g = max_{n in g} ||w_n||, B_g = max |b_n|
-// CEPS = 0.0085 adds ~7% slack (norms are fp32 and inflated by 1e-5); the EPS_ABS term bounds
-// 2^-17 |A| >= the bias-addition roundings plus the < 32-ulp truncation of the screened values
-// that carries the arg-max in their low bits (|A| <= ||u|| ||w_n|| (1 + 2^-7) + |b_n|).  A column
-// n is a candidate iff A_n + E >= max_m (A_m - E): every column holding the exact-fp32 maximum
-// passes, every rejected column is strictly below it.
-constexpr float CEPS = 0.0085f;
+// L = fl(sum_k u_k w_k) + b and the screen computes A = fl(sum_k bf16(u_k) bf16(w_k)) + b (the
+// bf16 x bf16 products are exact in fp32).  With du = u - bf16(u), dw = w - bf16(w):
+//   sum bf16(u) bf16(w) - sum u w = sum du_k bf16(w_k) + sum u_k dw_k
+//   => |.| <= ||du||_2 ||bf16(w)||_2 + ||u||_2 ||dw||_2            (Cauchy-Schwarz, exact reals)
+// and both fp32 accumulations add <= gamma_H sum|terms| each (MFMA: gamma_512 ~ 3.1e-5 times
+// ||bf16(u)|| ||bf16(w)|| <= (1 + 2^-8)^2 ||u|| ||w||; the rescoring's 8 chains of 64: gamma_67 ~
+// 4e-6 ||u|| ||w||).  ||du|| comes from the attention kernel that rounds u (the exact differences,
+// Sterbenz), ||dw_n|| from the pack; ||bf16(w)|| <= (1 + 2^-8) ||w||.  The screen applies one bound
+// per (row, 32-column granule g):
+//   E = SC_BF (||du|| W_g + ||u|| D_g) + SC_ACC ||u|| W_g + EPS_ABS (||u|| W_g + B_g),
+//   W_g = max_{n in g} ||w_n||, D_g = max ||dw_n||, B_g = max |b_n|
+// SC_BF = 1.005 >= (1 + 2^-8) with the fp32 norms' own rounding (norms inflated at the source);
+// SC_ACC = 5e-5 >= 3.1e-5 + 4e-6 with slack; the EPS_ABS term bounds 2^-17 |A| >= the
+// bias-addition roundings plus the < 32-ulp truncation of the screened values that carries the
+// arg-max in their low bits (|A| <= ||u|| ||w_n|| (1 + 2^-7) + |b_n|).  The rounding errors are
+// about 2^-10 relative on average against the worst case 2^-8 per operand, so E is ~2.5x below the
+// Cauchy-Schwarz bound on the worst case used before (0.0085 ||u|| W_g): fewer candidates for the
+// exact rescoring (tools/screen_candidates.py: mean 7.2 -> 2.5 per row, 32-column expansions 10x
+// rarer).  A column n is a candidate iff A_n + E >= max_m (A_m - E): every column holding the
+// exact-fp32 maximum passes, every rejected column is strictly below it.
+constexpr float SC_BF = 1.005f, SC_ACC = 5e-5f;
 constexpr float EPS_ABS = 1e-5f;
+// un = (||u||, ||u - bf16(u)||) of the row, g = (W_g, B_g, D_g, -) of the granule, all inflated at
+// their source over their own fp32 rounding
+__device__ __forceinline__ float screen_bound(float2 un, float4 g) {
+  const float uw = un.x * g.x;
+  return SC_BF * (un.y * g.x + un.x * g.z) + SC_ACC * uw + EPS_ABS * (uw + g.y);
+}
 constexpr int VS_TILE = 32;     // screen summary granule: one (lbmax, top-2 ub) per row per 32 columns
 constexpr int RS_CAP = 2048;    // candidate list capacity per row in k_vrescore (else full row)
 // Exact fp32 logits (k_vocab and the rescoring) are NP_VOCAB independent fma chains over contiguous
@@ -97,8 +111,8 @@ static Layout make_layout(const aa_dims& d) {
   L.mlp_w = take((size_t)L.Vp * L.H);
   L.mlp_b = take(L.Vp);
   L.mlp_wb = take((size_t)L.Vp * L.H / 2);  // bf16
-  L.mlp_wn = take(L.Vp);
-  L.mlp_gs = take((size_t)2 * (L.Vp / VS_TILE));  // float2 per granule: (max ||w_n||, max |b_n|)
+  L.mlp_wn = take((size_t)2 * L.Vp);  // ||w_n|| then ||w_n - bf16(w_n)|| (inflated)
+  L.mlp_gs = take((size_t)4 * (L.Vp / VS_TILE));  // float4 per granule: (max ||w_n||, max |b_n|, max ||dw_n||, 0)
   L.wgs = take((size_t)(L.H / 16) * 2 * P * 16);  // [tile][98][16]: W_g rows then W_s rows, 16 units of the tile
   L.mlp_w3 = take((size_t)3 * L.Vp * L.H / 2);    // W_m as 3 bf16 planes, fragments [Vp/32][H/16][3][64][8] (beam)
   L.enc_w4 = take((size_t)3 * L.H * L.C / 2);     // W_a as 3 bf16 planes, 16x16x32 fragments [H/16][C/32][3][64][8]
@@ -113,7 +127,7 @@ struct MP {  // resolved device pointers of the packed weights
   const bf16x8 *enc_w3, *whh3, *mlp_w3, *enc_w4, *heads_w4, *wvg4, *wv4;
   const float *enc_a_w, *enc_a_b, *heads_w, *heads_b, *wv, *wg, *ws, *wh, *whh, *wemb, *wvg, *bias5, *table, *mlp_w,
       *mlp_b, *mlp_wn, *wgs;
-  const float2* mlp_gs;
+  const float4* mlp_gs;
   const uint16_t* mlp_wb;
 };
 
@@ -133,7 +147,7 @@ static MP resolve(const aa_model* m, const Layout& L) {
   p.whh = b + L.whh; p.wemb = b + L.wemb; p.wvg = b + L.wvg; p.bias5 = b + L.bias5; p.table = b + L.table;
   p.mlp_w = b + L.mlp_w; p.mlp_b = b + L.mlp_b;
   p.mlp_wb = reinterpret_cast<const uint16_t*>(b + L.mlp_wb); p.mlp_wn = b + L.mlp_wn; p.wgs = b + L.wgs;
-  p.mlp_gs = reinterpret_cast<const float2*>(b + L.mlp_gs);
+  p.mlp_gs = reinterpret_cast<const float4*>(b + L.mlp_gs);
   return p;
 }
 
@@ -440,7 +454,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #ifndef AA_ENC4_NW
 #define AA_ENC4_NW 16
 #endif
-template <int NCB, int NW = 8>
+#ifndef AA_ENC4_WDB
+#define AA_ENC4_WDB 0
+#endif
+// WDB: the W fragments of stage s + 1 are loaded at the START of stage s into a second register set
+// (a whole stage of MFMAs to land), instead of after each column pair's last MFMA of stage s.
+template <int NCB, int NW = 8, bool WDB = false>
 __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ feats, int B, int C,
                                                 const bf16x8* __restrict__ W4, const float* __restrict__ bias,
                                                 float* __restrict__ V, float* __restrict__ a_g) {
@@ -471,7 +490,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);
   const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;  // block nb = wave NCB + c
   float ra[8];
-  bf16x8 wv[NCB][3];
+  bf16x8 wv0[NCB][3], wv1[WDB ? NCB : 1][3];
   floatx4 acc[E4_RB][NCB];
 #pragma unroll
   for (int rb = 0; rb < E4_RB; ++rb)
@@ -483,7 +502,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
 #pragma unroll
     for (int i = 0; i < 8; ++i) ra[i] = AA_FEAT_LOAD(src + i * P);
   };
-  auto gload_w = [&](int s, int c) {
+  auto gload_w = [&](int s, int c, bf16x8 (&wv)[NCB][3]) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)s * 3 + q) * 64];
   };
@@ -506,18 +525,36 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   };
 
   const int ns = KC;
-  if (stg) gload_a(0);
+  if constexpr (WDB) {
+    // prologue in the loop's steady-state load order (A of the next stage, then this stage's W
+    // youngest), so the waits at the loop head can count instead of draining
+    if (stg) {
+      gload_a(0);
+      lstore_a(0);
+      gload_a(ns > 1 ? 1 : 0);
+    }
 #pragma unroll
-  for (int c = 0; c < NCB; ++c) gload_w(0, c);
-  if (stg) lstore_a(0);
-  if (stg) gload_a(ns > 1 ? 1 : 0);
+    for (int c = 0; c < NCB; ++c) gload_w(0, c, wv0);
+  } else {
+    if (stg) gload_a(0);
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) gload_w(0, c, wv0);
+    if (stg) lstore_a(0);
+    if (stg) gload_a(ns > 1 ? 1 : 0);
+  }
   __syncthreads();
-  for (int s = 0; s < ns; ++s) {
+  // one 32-channel stage; wv: this stage's W fragments, wn: the next stage's (WDB) -- the stage loop
+  // below runs stages in pairs with the two register sets swapped, so both stay statically indexed
+  auto stage = [&](int s, bf16x8 (&wv)[NCB][3], bf16x8 (&wn)[NCB][3]) {
     const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
     // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
     if (stg) {
       lstore_a(buf ^ 1);
       gload_a(s2);
+    }
+    if constexpr (WDB) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) gload_w(s1, c, wn);
     }
     __builtin_amdgcn_sched_barrier(0);
     const __bf16* Ab = &As[buf][0][fo];
@@ -549,8 +586,10 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
           acc[rb][c1] = y;
         }
       }
-      gload_w(s1, 2 * cp);
-      gload_w(s1, 2 * cp + 1);
+      if constexpr (!WDB) {
+        gload_w(s1, 2 * cp, wv);
+        gload_w(s1, 2 * cp + 1, wv);
+      }
       // re-read the A fragments for the next pair instead of keeping all 21 live (VGPR budget)
       asm volatile("" ::: "memory");
     }
@@ -569,6 +608,16 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
     }
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (WDB) {
+    int s = 0;
+    for (; s + 1 < ns; s += 2) {
+      stage(s, wv0, wv1);
+      stage(s + 1, wv1, wv0);
+    }
+    if (s < ns) stage(s, wv0, wv1);
+  } else {
+    for (int s = 0; s < ns; ++s) stage(s, wv0, wv0);
   }
   // a_g of the workgroup's images (the last workgroup of an odd batch holds one)
   for (int i = t; i < 2 * C; i += NT) {
@@ -950,12 +999,26 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-template <int H, int NG = LS_GATHERS, class F>
+// Two more hooks for the fused-rescoring launch (k_lstm<.., RS>), both inside the ring at fixed
+// iterations so every wait stays a compile-time count: at iteration JK (after that iteration's
+// stage issue) `kdma` lets wave 0 issue ONE more LDS-DMA (the tile's published keys); at iteration JG
+// >= JK + NB (by then that DMA has landed: it is older than the stage the iteration waits for)
+// `mid` may read it from LDS and issue exactly NG2 ordinary loads per wave (the token-dependent
+// table gathers), which land under the remaining iterations.  JK < 0: no hooks.
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <int H, int NG = LS_GATHERS, int JK = -1, int JG = -1, int NG2 = 0, class F, class FK = NoHook,
+          class FM = NoHook>
 __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* af1, const bf16x8* wf0,
-                                              const bf16x8* wf1, bf16x8* stg, float* Pt, F&& pre) {
+                                              const bf16x8* wf1, bf16x8* stg, float* Pt, F&& pre,
+                                              FK&& kdma = FK{}, FM&& mid = FM{}) {
   constexpr int KC = H / 16, CP = LS_CP, N = KC / 2, NB = LS_NB < N ? LS_NB : N;
   constexpr int LS_GATHERS = NG;  // ordinary loads `pre` issues (0: none)
   static_assert(NB >= 3, "the ring needs at least three stages");
+  static_assert(JK < 0 || (JK + NB < N - 1 && JG >= JK + NB && JG < N - 1), "hook iterations");
+  // last stage issued before each hook's loads (they are younger than it, older than the next)
+  constexpr int SK = JK + NB < N - 1 ? JK + NB : N - 1, SG = JG + NB < N - 1 ? JG + NB : N - 1;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int a = (wave >> 1) & 1, c = wave & 1, kh = wave >> 2;
   const bf16x8* src[3];
@@ -1002,10 +1065,25 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
       // stage it + 1 landed: younger are the stages issued after it (up to it + NB - 1) and, while
       // it + 1 <= NB - 1, the gathers (issued after stage NB - 1)
       const int last = it + NB - 1 < N - 1 ? it + NB - 1 : N - 1;
-      vm_wait(3 * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0));
+      int younger = 3 * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0);
+      if (JK >= 0 && it >= JG + 1 && it + 1 <= SG) younger += NG2;
+      if (JK >= 0 && it >= JK + 1 && it + 1 <= SK && wave == 0) younger += 1;
+      vm_wait(younger);
       // every wave's stage-it reads retired (lgkmcnt) before any wave refills that buffer
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (it + NB < N) issue(it + NB);
+      if constexpr (JK >= 0) {
+        if (it == JK) {
+          __builtin_amdgcn_sched_barrier(0);
+          kdma();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (it == JG) {
+          __builtin_amdgcn_sched_barrier(0);
+          mid();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       lread(it + 1, set ^ 1);
     }
     x3_step2(acc2, acc, fa[set], fw[set]);
@@ -1064,6 +1142,16 @@ __device__ __forceinline__ uint64_t rescore_row(int b, bool write, int t, int V,
                                                 const float* __restrict__ bias, uint64_t* __restrict__ keys,
                                                 int64_t* __restrict__ ids, int T, int t_step, float* scr);
 constexpr uint64_t RS_WAIT_TICKS = 5000;  // 50 us of the 100 MHz constant clock
+#ifndef AA_RS_PRIO
+#define AA_RS_PRIO 0
+#endif
+// ring iterations (of H / 32) at which k_lstm<.., RS> DMAs the tile's keys and gathers the table rows
+#ifndef LS_RS_JK
+#define LS_RS_JK 10
+#endif
+#ifndef LS_RS_JG
+#define LS_RS_JG (LS_RS_JK + 3)
+#endif
 template <int H, bool G = false, bool RS = false>
 __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
@@ -1077,7 +1165,9 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
   AA_TS(0, 0);
   // the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
   constexpr int RING_FLOATS = (LS_NB < H / 32 ? LS_NB : H / 32) * LS_STAGE * 4;
-  constexpr int LDS_FLOATS = RING_FLOATS + 64 + 4;  // + the tile's 64 tokens (+ RS: the missing-row mask)
+  // + the tile's 64 tokens (+ RS: the missing-row mask and slow-path flag, the 64 keys' low words
+  // DMA'd mid-ring)
+  constexpr int LDS_FLOATS = RING_FLOATS + 64 + 4 + (RS ? 64 : 0);
   static_assert(TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
@@ -1087,9 +1177,14 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
     static_assert(!G, "the fused rescoring is the greedy path's");
     static_assert(TS + 2 * RsScratch<H>::FLOATS <= RING_FLOATS, "two rescoring scratch areas beside the tile");
     if (bid < ra.NR) {  // rescoring role (uniform per workgroup): rows 2 bid + (t >> 8)
+      AA_TS(4, 0);
+#if AA_RS_PRIO
+      __builtin_amdgcn_s_setprio(AA_RS_PRIO);  // its dependent loads ahead of the GEMM ring's on the CU
+#endif
       const int row = 2 * bid + (int)(threadIdx.x >> 8);
       rescore_row<H, true>(row < B ? row : B - 1, row < B, threadIdx.x & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
                            ra.bias, ra.keys, ra.ids, ra.T, ra.t_step, lds + (threadIdx.x >> 8) * RsScratch<H>::FLOATS);
+      AA_TS(4, 1);
       return;
     }
     bid -= ra.NR;
@@ -1134,63 +1229,102 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
   // epilogue gathers behind the first GEMM loads: token -> table row, x_g, c, W_g/W_s slice
   float2 ta[4], xa[4], sa, sb, cprev;
   float4 wsv;
-  auto gathers = [&] {
+  const int N5 = 5 * H;
+  // the token's table row (5 loads)
+  auto gather_table = [&] {
     tk = tk < 0 ? 0 : (tk >= V ? V - 1 : tk);
-    const int N5 = 5 * H;
     const float* trow = table + tk * N5;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
+    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+  };
+  // the token-independent operands: x_g, c, the W_g / W_s slice (7 loads)
+  auto gather_x = [&] {
     const float* xrow = xg + (int64_t)mc * N5;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      ta[g] = *reinterpret_cast<const float2*>(trow + nt * 64 + g * 16 + u0);
-      xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
-    }
-    sa = *reinterpret_cast<const float2*>(trow + 4 * H + j);
+    for (int g = 0; g < 4; ++g) xa[g] = *reinterpret_cast<const float2*>(xrow + nt * 64 + g * 16 + u0);
     sb = *reinterpret_cast<const float2*>(xrow + 4 * H + j);
     cprev = *reinterpret_cast<const float2*>(c_in + (int64_t)pc * H + j);
     // W_g / W_s slice: wgs[tile] is [98][16] (j-major); thread t < 392 takes float4 t
     const float4* src = reinterpret_cast<const float4*>(wgs + (int64_t)nt * 2 * P * 16);
     wsv = src[t < 2 * P * 4 ? t : 2 * P * 4 - 1];
   };
+  auto gathers = [&] {
+    gather_table();
+    gather_x();
+  };
   // token first (oldest), then the ring's first three stages, then -- once the token is in --
   // the token-dependent gathers (exactly LS_GATHERS loads, counted by the ring's waits)
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (RS) {
-    // the GEMM phase alone (no token yet), then the keys of the tile's rows, then the gathers
-    lstm_gemm_lds<H, 0>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [] {});
+    // The GEMM phase needs no token.  At ring iteration LS_RS_JK wave 0 DMAs the low words of the
+    // tile's 64 keys into LDS (agent-coherent sc1 reads of the granules the rescoring workgroups
+    // publish: a non-zero low word = published, it is 0xFFFFFFFF - token), and at iteration LS_RS_JG
+    // -- that DMA landed -- every thread takes its row's token if published and issues all twelve
+    // gathers (table row, x_g, c, W_g / W_s slice: issued there rather than with the first stages, so
+    // they are not live across the whole ring), which land under the last iterations.  Rows not yet published then are polled / rescored after the ring, as before,
+    // and only their table rows are gathered again.
+    uint32_t* klo = reinterpret_cast<uint32_t*>(lds + RING_FLOATS + 64 + 4);
+    // (hooks scaled to the ring's H / 32 iterations; rings under 12 iterations: gathers after the ring)
+    constexpr int NI = H / 32, JK = NI >= 12 ? LS_RS_JK * NI / 16 : -1, JG = JK < 0 ? -1 : JK + (LS_RS_JG - LS_RS_JK);
+    lstm_gemm_lds<H, 0, JK, JG, 12>(
+        af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [] {},
+        [&] {
+          if (t < 64) {
+            const int r = m0 + t < B ? m0 + t : B - 1;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ra.keys + r),
+                                             (__attribute__((address_space(3))) void*)klo, 4, 0, 16 /* sc1 */);
+          }
+        },
+        [&] {
+          const uint32_t kl = klo[rr];
+          tk = kl != 0u ? (int64_t)(0xFFFFFFFFu - kl) : 0;  // not yet published: gathered again below
+          gathers();
+        });
+    AA_TS(0, 5);
     __syncthreads();
     uint64_t* miss = reinterpret_cast<uint64_t*>(lds + RING_FLOATS + 64);
     if (t < 64) {
-      const int r = m0 + t < B ? m0 + t : B - 1;
-      uint64_t k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t t0 = wall_clock64();
-      while (!__all(k != 0)) {  // wave-uniform: bounded poll of the 8-byte granules
-        if (wall_clock64() - t0 > ra.wait) break;
-        __builtin_amdgcn_s_sleep(1);
-        if (k == 0) k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t kl = JK < 0 ? 0u : klo[t];
+      if (__all(kl != 0u)) {  // wave-uniform: every row was published by iteration JK
+        if (t == 0) miss[0] = 0, miss[1] = 0;
+      } else {
+        const int r = m0 + t < B ? m0 + t : B - 1;
+        uint64_t k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = wall_clock64();
+        while (!__all(k != 0)) {  // wave-uniform: bounded poll of the 8-byte granules
+          if (wall_clock64() - t0 > ra.wait) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (k == 0) k = __hip_atomic_load(ra.keys + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        tok_lds[t] = (int)key_token(k);
+        const uint64_t mb = __ballot(k == 0);
+        if (t == 0) miss[0] = mb, miss[1] = 1;
       }
-      tok_lds[t] = (int)key_token(k);
-      const uint64_t mb = __ballot(k == 0);
-      if (t == 0) *miss = mb;
     }
     __syncthreads();
-    uint64_t mb = *miss;
-    // rows not yet published: rescored here, two at a time (the tile's Pt stays below the scratch)
-    while (mb) {
-      const int i0 = __builtin_ctzll(mb);
-      mb &= mb - 1;
-      const int i1 = mb ? __builtin_ctzll(mb) : i0;
-      if (mb) mb &= mb - 1;
-      const int i = (t >> 8) ? i1 : i0;
-      const int r = m0 + i < B ? m0 + i : B - 1;
-      const uint64_t k = rescore_row<H, true>(r, (t >> 8) == 0 || i1 != i0, t & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
-                                              ra.bias, ra.keys, ra.ids, ra.T, ra.t_step,
-                                              lds + TS + (t >> 8) * RsScratch<H>::FLOATS);
-      if ((t & 255) == 0) tok_lds[i] = (int)key_token(k);
-      __syncthreads();
+    if (miss[1]) {  // (workgroup-uniform) some key came after iteration JK: the slow path
+      uint64_t mb = miss[0];
+      // rows not yet published: rescored here, two at a time (the tile's Pt stays below the scratch)
+      while (mb) {
+        const int i0 = __builtin_ctzll(mb);
+        mb &= mb - 1;
+        const int i1 = mb ? __builtin_ctzll(mb) : i0;
+        if (mb) mb &= mb - 1;
+        const int i = (t >> 8) ? i1 : i0;
+        const int r = m0 + i < B ? m0 + i : B - 1;
+        const uint64_t k = rescore_row<H, true>(r, (t >> 8) == 0 || i1 != i0, t & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
+                                                ra.bias, ra.keys, ra.ids, ra.T, ra.t_step,
+                                                lds + TS + (t >> 8) * RsScratch<H>::FLOATS);
+        if ((t & 255) == 0) tok_lds[i] = (int)key_token(k);
+        __syncthreads();
+      }
+      // every gather again (the mid-ring values are dead on this path, so they are not kept live
+      // across the rescoring above)
+      tk = tok_lds[rr];
+      gathers();
     }
-    tk = tok_lds[rr];
-    gathers();
   } else {
     lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
       // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
@@ -1280,7 +1414,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   __shared__ float zs[PP];
   __shared__ float sh_alpha[PP];
   __shared__ float sh_beta;
-  __shared__ float sh_norm[4];
+  __shared__ float sh_norm[8];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = blockIdx.x;
   // ---- loads independent of alpha, oldest first in the order they are consumed ------------------
@@ -1366,7 +1500,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   __syncthreads();
   // 4) context + u
   const float beta = sh_beta;
-  float nsq = 0.f;
+  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
 #pragma unroll
   for (int i = 0; i < HPT; ++i) {
     const int d = t + 256 * i;
@@ -1377,7 +1511,12 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
     const float u = chat + hv[i];
     nsq = __builtin_fmaf(u, u, nsq);
     u_out[(int64_t)b * H + d] = u;
-    if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+    if (ub_out) {
+      const uint16_t ubv = f2bf(u);
+      ub_out[frag_off(b, d, H)] = ubv;
+      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
+      dsq = __builtin_fmaf(du, du, dsq);
+    }
     if (ub3_out) {  // u as 3 bf16 planes in fragment order (beam search's bf16x3 vocab GEMM)
       __bf16 x0, x1, x2;
       split3(u, x0, x1, x2);
@@ -1388,11 +1527,15 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
       o[128 * 8] = x2;
     }
   }
-  if (unorm) {
+  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
     nsq = wave_sum(nsq);
-    if (lane == 0) sh_norm[w] = nsq;
+    dsq = wave_sum(dsq);
+    if (lane == 0) sh_norm[w] = nsq, sh_norm[4 + w] = dsq;
     __syncthreads();
-    if (t == 0) unorm[b] = sqrtf((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) * 1.00001f;
+    if (t == 0) {
+      unorm[b] = sqrtf((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) * 1.0001f;
+      unorm[B + b] = sqrtf((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7])) * 1.0001f;
+    }
   }
 }
 
@@ -1401,6 +1544,9 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
 // flight per CU), the 32 projection partials summed by four groups of 128 threads (8 each, then
 // (g0 + g1) + (g2 + g3)), and each of the 50 scores by 8 lanes (7 terms each, xor-butterfly
 // combine).  Same outputs as k_atten; rounding of the projections / scores differs (fixed orders).
+#ifndef AA_ATTEN_PRIO
+#define AA_ATTEN_PRIO 0
+#endif
 template <int H>
 __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __restrict__ h_new,
                                                 const float* __restrict__ s_new, const float* __restrict__ part,
@@ -1415,8 +1561,13 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   __shared__ float zs[PP];
   __shared__ float sh_alpha[PP];
   __shared__ float sh_beta;
-  __shared__ float sh_norm[8];
+  __shared__ float sh_norm[16];
   AA_TS(1, 0);
+#if AA_ATTEN_PRIO
+  // the small loads at a raised wave priority, V at the normal one: the CU issues every wave's small
+  // loads before any wave's V stream
+  __builtin_amdgcn_s_setprio(AA_ATTEN_PRIO);
+#endif
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
@@ -1446,6 +1597,10 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
 #define AA_ATTEN_VA P
 #endif
   constexpr int VA = AA_ATTEN_VA < P ? AA_ATTEN_VA : P;
+#if AA_ATTEN_PRIO
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
   for (int i = 0; i < DPT; ++i)
 #pragma unroll
@@ -1516,7 +1671,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   AA_TS(1, 3);
   // 4) context + u
   const float beta = sh_beta;
-  float nsq = 0.f;
+  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
 #pragma unroll
   for (int i = 0; i < DPT; ++i) {
     const int d = t + 512 * i;
@@ -1527,7 +1682,12 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
     const float u = chat + hv[i];
     nsq = __builtin_fmaf(u, u, nsq);
     u_out[(int64_t)b * H + d] = u;
-    if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+    if (ub_out) {
+      const uint16_t ubv = f2bf(u);
+      ub_out[frag_off(b, d, H)] = ubv;
+      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
+      dsq = __builtin_fmaf(du, du, dsq);
+    }
     if (ub3_out) {
       __bf16 x0, x1, x2;
       split3(u, x0, x1, x2);
@@ -1538,13 +1698,17 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
       o[128 * 8] = x2;
     }
   }
-  if (unorm) {
+  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
     nsq = wave_sum(nsq);
-    if (lane == 0) sh_norm[w] = nsq;
+    dsq = wave_sum(dsq);
+    if (lane == 0) sh_norm[w] = nsq, sh_norm[8 + w] = dsq;
     __syncthreads();
-    if (t == 0)
+    if (t == 0) {
       unorm[b] = sqrtf(((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) +
-                       ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.00001f;
+                       ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.0001f;
+      unorm[B + b] = sqrtf(((sh_norm[8] + sh_norm[9]) + (sh_norm[10] + sh_norm[11])) +
+                           ((sh_norm[12] + sh_norm[13]) + (sh_norm[14] + sh_norm[15]))) * 1.0001f;
+    }
   }
   AA_TS(1, 4);
 }
@@ -1698,7 +1862,7 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
 
 // ---------------------------------------------------------------------------------------------
 // D3a (greedy path): vocab screen.  bf16 MFMA logits A_n = bf16(u) . bf16(w_n) + b_n over a
-// 128x128 tile, then per (row, 32-column granule g) with the granule's bound E (see CEPS):
+// 128x128 tile, then per (row, 32-column granule g) with the granule's bound E (see screen_bound):
 //   summ[row][g] = {max_n A_n - E, max_n A_n + E, second largest A_n + E, arg-max column}.
 // ---------------------------------------------------------------------------------------------
 // Partner exchange for the screen epilogue's butterfly over the 32 lanes of a column block: level
@@ -1744,11 +1908,11 @@ constexpr int SC_BM = 64, SC_BN = 64, SC_PT = 64 * 68;  // partial tile, pitch 6
 template <int H>
 __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const bf16x8* __restrict__ ua,
                                                     const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                                    const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                    const float4* __restrict__ gs, const float* __restrict__ bias,
                                                     float4* __restrict__ summ) {
   constexpr int KC = H / 16, KW = KC / 4;  // k16 chunks per wave
   __shared__ __attribute__((aligned(16))) float Pt[2 * SC_PT];
-  __shared__ float un_s[SC_BM];
+  __shared__ float2 un_s[SC_BM];
   const int NTn = Vp / VS_TILE, NTs = Vp / SC_BN, MT = (B + SC_BM - 1) / SC_BM;
   const int L = xcd_remap(blockIdx.x, MT * NTs);
   const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
@@ -1766,11 +1930,12 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const 
       fw[c][x] = w0[((size_t)x * KC + c) * 64];
     }
   // epilogue operands, loaded behind the fragments (their latency hides under the MFMAs)
-  const float unv = unorm[m0 + (t & 63) < B ? m0 + (t & 63) : B - 1];
+  const int ur = m0 + (t & 63) < B ? m0 + (t & 63) : B - 1;
+  const float2 unv = make_float2(unorm[ur], unorm[B + ur]);
   const int wm = wave >> 1, wn_ = wave & 1;
   const int col = n0 + wn_ * 32 + li;
   const float bv = bias[col];
-  const float2 gsv = gs[(n0 + wn_ * 32) / VS_TILE];
+  const float4 gsv = gs[(n0 + wn_ * 32) / VS_TILE];
   floatx16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1858,8 +2023,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const 
       if (!(li & 1) && row < B) {
         float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
         if (m1) {
-          const float un = un_s[rl], uw = un * gsv.x;
-          const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+          const float E = screen_bound(un_s[rl], gsv);
           const float x1 = key_value(m1 & ~31u);
           const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
           o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + c) * VS_TILE + (int)(m1 & 31u)));
@@ -1884,8 +2048,8 @@ constexpr int SC2_STAGE = SC2_NB * SC2_KS * 64;  // bf16x8 per LDS stage (20 KB)
 
 // Per (row, granule) summary of one 32 x 32 block of screened logits in MFMA C layout (rows row0..,
 // columns 32 G..): keys, transposing top-2 butterfly, bound E, one float4 per row (see k_vscreen).
-__device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0, int G, float bv, float2 gsv,
-                                                  const float* __restrict__ un_blk, bool valid, int B, int NTn,
+__device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0, int G, float bv, float4 gsv,
+                                                  const float2* __restrict__ un_blk, bool valid, int B, int NTn,
                                                   float4* __restrict__ summ) {
   const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
   uint32_t k1[16], k2[16];
@@ -1909,8 +2073,7 @@ __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0,
   if (!(li & 1) && row < B) {
     float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
     if (m1) {
-      const float uw = un_blk[rl] * gsv.x;
-      const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+      const float E = screen_bound(un_blk[rl], gsv);
       const float x1 = key_value(m1 & ~31u);
       const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
       o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float(G * VS_TILE + (int)(m1 & 31u)));
@@ -1961,7 +2124,7 @@ __device__ __forceinline__ void screen_bfly16_swap(uint32_t (&k1)[16], uint32_t 
 
 template <int NB>
 __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], int row0, int G0, const float (&bv)[NB],
-                                                   const float2* __restrict__ gsb, const float* __restrict__ un_blk,
+                                                   const float4* __restrict__ gsb, const float2* __restrict__ un_blk,
                                                    int c0, int V, int B, int NTn, float4* __restrict__ summ) {
   const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
   uint32_t k1[NB][16], k2[NB][16];
@@ -1986,7 +2149,7 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
   const int rr = (li >> 1) & 15;  // this lane pair now holds row acc_row(rr) of each block
   const int rl = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
   const int row = row0 + rl;
-  const float uw0 = un_blk[rl];
+  const float2 uw0 = un_blk[rl];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const uint32_t r1 = partner<1>(k1[b][0]), r2 = partner<1>(k2[b][0]);
@@ -1996,9 +2159,7 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
     if (!(li & 1) && row < B) {
       float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
       if (m1) {
-        const float2 gsv = gsb[b];
-        const float uw = uw0 * gsv.x;
-        const float E = CEPS * uw + EPS_ABS * (uw + gsv.y);
+        const float E = screen_bound(uw0, gsb[b]);
         const float x1 = key_value(m1 & ~31u);
         const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
         o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + b) * VS_TILE + (int)(m1 & 31u)));
@@ -2014,8 +2175,8 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
 template <int H>
 __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8* __restrict__ ua,
                                              const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                             bf16x8 (*Ws)[SC2_STAGE], float* un_s, floatx16 (&acc)[SC2_NB],
-                                             const float2* __restrict__ gs = nullptr, float2* gs_s = nullptr) {
+                                             bf16x8 (*Ws)[SC2_STAGE], float2* un_s, floatx16 (&acc)[SC2_NB],
+                                             const float4* __restrict__ gs = nullptr, float4* gs_s = nullptr) {
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = SC2_STAGE / 256;  // bf16x8 per thread per stage
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   // this wave's u fragments (row block m0 / 32 + wave) and the W stages arrive AA_SCREEN_AHEAD stages
@@ -2060,7 +2221,7 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
   // those stages, which the first MFMAs wait for anyway)
   if (t < SC2_BM) {
     const int r = m0 + t;
-    un_s[t] = unorm[r < B ? r : B - 1];
+    un_s[t] = make_float2(unorm[r < B ? r : B - 1], unorm[B + (r < B ? r : B - 1)]);
   } else if (gs_s && t < SC2_BM + SC2_NB) {  // the granule bound factors, staged with ||u||
     gs_s[t - SC2_BM] = gs[n0 / VS_TILE + t - SC2_BM];
   }
@@ -2084,14 +2245,17 @@ __device__ __forceinline__ void screen2_main(int B, int m0, int n0, const bf16x8
   }
 }
 
+#ifndef AA_SCREEN_OCC
+#define AA_SCREEN_OCC 2
+#endif
 template <int H>
-__global__ __launch_bounds__(256, 2) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+__global__ __launch_bounds__(256, AA_SCREEN_OCC) void k_vscreen2(int B, int V, int Vp, const bf16x8* __restrict__ ua,
                                                   const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
-                                                  const float2* __restrict__ gs, const float* __restrict__ bias,
+                                                  const float4* __restrict__ gs, const float* __restrict__ bias,
                                                   float4* __restrict__ summ) {
   __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
-  __shared__ float un_s[SC2_BM];
-  __shared__ float2 gs_s[SC2_NB];
+  __shared__ float2 un_s[SC2_BM];
+  __shared__ float4 gs_s[SC2_NB];
   AA_TS(2, 0);
   const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
   const int L = xcd_remap(blockIdx.x, MT * NT);
@@ -2424,25 +2588,36 @@ __global__ void k_pack_wgs(const float* __restrict__ wg, const float* __restrict
   }
 }
 
-// bf16 copy of W_m (zero rows beyond V) and inflated row norms ||w_n||_2 for the screen bound.
-__global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, uint16_t* __restrict__ wb, float* __restrict__ wn) {
+// bf16 copy of W_m (zero rows beyond V) and, for the screen bound, the row norms ||w_n||_2 (wn[n])
+// and ||w_n - bf16(w_n)||_2 (wn[Vp + n]), each inflated by 1e-4 over its fp32 rounding (a sum of
+// H <= 1024 squares: relative error <= gamma_1024 ~ 6.1e-5, then the square root).
+__global__ void k_pack_mlp(const float* __restrict__ w, int V, int H, int Vp, uint16_t* __restrict__ wb,
+                           float* __restrict__ wn) {
   const int n = blockIdx.x, lane = threadIdx.x;  // 64 threads
-  float s = 0.f;
+  float s = 0.f, sd = 0.f;
   for (int k = lane; k < H; k += 64) {
     const float x = n < V ? w[(int64_t)n * H + k] : 0.f;
-    wb[frag_off(n, k, H)] = f2bf(x);
-    s += x * x;
+    const uint16_t xb = f2bf(x);
+    wb[frag_off(n, k, H)] = xb;
+    const float d = x - __uint_as_float((uint32_t)xb << 16);  // exact (Sterbenz)
+    s = __builtin_fmaf(x, x, s);
+    sd = __builtin_fmaf(d, d, sd);
   }
   s = wave_sum(s);
-  if (lane == 0) wn[n] = sqrtf(s) * 1.00001f;
+  sd = wave_sum(sd);
+  if (lane == 0) {
+    wn[n] = sqrtf(s) * 1.0001f;
+    wn[Vp + n] = sqrtf(sd) * 1.0001f;
+  }
 }
 
-// Per 32-column granule of the vocab: (max_n ||w_n||, max_n |b_n|) for the screen's bound.
-__global__ void k_pack_gs(const float* __restrict__ wn, const float* __restrict__ b, float2* __restrict__ gs) {
+// Per 32-column granule of the vocab: (max ||w_n||, max |b_n|, max ||w_n - bf16(w_n)||, 0) for the
+// screen's bound.
+__global__ void k_pack_gs(const float* __restrict__ wn, const float* __restrict__ b, int Vp, float4* __restrict__ gs) {
   const int g = blockIdx.x, l = threadIdx.x;  // 64 threads, lanes >= 32 mirror 0..31
   const int n = g * VS_TILE + (l & (VS_TILE - 1));
-  const float mw = wave_max(wn[n]), mb = wave_max(fabsf(b[n]));
-  if (l == 0) gs[g] = make_float2(mw, mb);
+  const float mw = wave_max(wn[n]), mb = wave_max(fabsf(b[n])), md = wave_max(wn[Vp + n]);
+  if (l == 0) gs[g] = make_float4(mw, mb, md, 0.f);
 }
 
 __device__ __forceinline__ uint64_t splitmix(uint64_t z) {
@@ -2555,10 +2730,10 @@ int aa_pack_weights(const aa_model* m, const aa_ref_weights* w, aa_stream_t stre
                      w->sent_affine_x_w, E, H, base + L.whh, base + L.wemb, base + L.wvg, base + L.bias5);
   // table[v] = embed[v] . [W_ih(emb part) (packed gate order); W_x(emb part)]^T
   gemm_bias(w->embed_w, E, V, base + L.wemb, E, L.N5, E, nullptr, base + L.table, L.N5, s);
-  hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H,
+  hipLaunchKernelGGL(k_pack_mlp, dim3(L.Vp), dim3(64), 0, s, base + L.mlp_w, V, H, L.Vp,
                      reinterpret_cast<uint16_t*>(base + L.mlp_wb), base + L.mlp_wn);
-  hipLaunchKernelGGL(k_pack_gs, dim3(L.Vp / VS_TILE), dim3(64), 0, s, base + L.mlp_wn, base + L.mlp_b,
-                     reinterpret_cast<float2*>(base + L.mlp_gs));
+  hipLaunchKernelGGL(k_pack_gs, dim3(L.Vp / VS_TILE), dim3(64), 0, s, base + L.mlp_wn, base + L.mlp_b, L.Vp,
+                     reinterpret_cast<float4*>(base + L.mlp_gs));
   hipLaunchKernelGGL(k_pack_wgs, dim3(H / 16), dim3(256), 0, s, w->att_affine_g_w, w->att_affine_s_w, H, base + L.wgs);
   hipLaunchKernelGGL(k_pack_w3, dim3((H / 32) * (C / 16)), dim3(64), 0, s, w->enc_affine_a_w, C,
                      reinterpret_cast<bf16x8*>(base + L.enc_w3));
@@ -2653,7 +2828,10 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     // k_enc_v4 computes V and a_g in one pass over the feature map; the a_g branch (heads, x_g)
     // then runs on aux beside the VWv GEMM.  (Trace: the fused avg-pool is a zero-length pair.)
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
-    if (H == 512)
+    if (H == 512 && AA_ENC4_WDB)
+      AA_TLAUNCH(ev, 2, (k_enc_v4<4, 8, true>), dim3(nwg), dim3(512), 0, s, feats, B, C, (const bf16x8*)p.enc_w4,
+                 (const float*)p.enc_a_b, V, a_g);
+    else if (H == 512)
       AA_TLAUNCH(ev, 2, (k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg), dim3(64 * AA_ENC4_NW), 0, s, feats, B, C,
                  (const bf16x8*)p.enc_w4, (const float*)p.enc_a_b, V, a_g);
     else
@@ -2774,7 +2952,7 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
   }
   w.s = c.take<float>((size_t)B * L.H);
   w.u = c.take<float>((size_t)B * L.H);
-  w.unorm = c.take<float>((size_t)B);
+  w.unorm = c.take<float>((size_t)2 * B);  // ||u|| then ||u - bf16(u)|| per row
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
   w.ub = c.take<uint16_t>((size_t)((B + 127) / 128) * 128 * L.H);  // fragment order, 128-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
@@ -2950,9 +3128,10 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
     float* blt = beta ? beta + t : nullptr;
     RsArgs ra{rup((B + 1) / 2, 8), L.Vp, T, t - 1, (flags & AA_DECODE_RS_SELF) ? 0 : RS_WAIT_TICKS, w.u, w.summ,
               p.mlp_w, p.mlp_b, kt - B, ids};
-    lstm_atten_launch(L, p, B, tok, tok_ld, w.V, w.vwv, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt], w.c[nxt],
-                      w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm, alt, (int64_t)T * P, blt,
-                      T, trace, t, s, nullptr, 1, nullptr, fused && t > 0 ? &ra : nullptr);
+    lstm_launch(L, p, B, tok, tok_ld, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt], w.c[nxt], w.s, w.part, s,
+                nullptr, fused && t > 0 ? &ra : nullptr, trace ? trace->lstm_events : nullptr, 2 * t);
+    atten_launch(L, p, B, w.V, w.vwv, w.h[nxt], w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
+                 alt, (int64_t)T * P, blt, T, s, 1, nullptr, trace ? trace->atten_events : nullptr, 2 * t);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     if (exact) {

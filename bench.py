@@ -348,6 +348,8 @@ def main():
                     "buffer (MALL-resident; not the metric)")
     ap.add_argument("--pool-streams", action="store_true", help="pipeline slots on torch pool streams instead of "
                     "freshly created HIP streams")
+    ap.add_argument("--decode-flags", type=int, default=0, help="diagnostics: extra aa_greedy_decode flags (e.g. "
+                    "1024 = AA_DECODE_SPLIT_RESCORE), as model.decode_extra_flags")
     ap.add_argument("--regions", type=int, default=5, help="timed regions per mode (median reported; >= 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cpu-plumbing", action="store_true", help="CPU tests only: run the N > 1 launch / gather / "
@@ -383,6 +385,7 @@ def main():
     # one process per GPU: this rank's sampler() stays on its own device (the single-process
     # multi-device mode, on by default when several GPUs are visible, is not what a rank measures)
     model.device_parallel = False
+    model.decode_extra_flags = args.decode_flags
     depth = max(1, args.pipeline_depth)
     # distinct resident feature batches: each batch in flight reads its own 205 MB
     # map, so nothing is served from the 256 MB MALL left behind by the previous batch.  Buffer 0 is
@@ -499,7 +502,7 @@ def main():
             for k, i in enc_pairs.items():
                 per[k].append(ev["encoder"].elapsed_ms(2 * i, 2 * i + 1))
             lstm = ev["lstm"].pair_durations_ms()
-            per["k_lstm(step0)"].append(lstm[0])  # step 0: no previous step to rescore
+            per["k_lstm(step0)"].append(lstm[0])  # step 0: GEMM + cell, no previous step to rescore
             per["k_lstm"] += lstm[1:]             # steps 1..T-1: + the rescoring of step t-1
             per["k_atten"] += ev["atten"].pair_durations_ms()
             per["k_vscreen"] += ev["screen"].pair_durations_ms()

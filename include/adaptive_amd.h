@@ -116,10 +116,13 @@ typedef struct aa_model {
 } aa_model;
 
 /* Optional per-kernel timing (hipEvent_t handles created by the caller), one array per kernel so
- * the averages line up with rocprofv3's per-kernel statistics.  For each non-NULL array,
- * aa_greedy_decode records event [2i] before and [2i+1] after the i-th launch of that kernel:
+ * the figures line up with rocprofv3's per-kernel statistics.  For each non-NULL array, the pair
+ * ([2i], [2i+1]) of the i-th launch of that kernel is handed to the launch itself
+ * (hipExtLaunchKernel start / stop events): it carries the dispatch's own begin / end timestamps,
+ * and no event packet sits between the traced launches:
  *   encoder_events: 2*AA_TRACE_ENCODER_KERNELS events, launches in the order
- *                   k_avgpool, k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM (k_gemm_bias);
+ *                   k_avgpool (not launched by k_enc_v4, which fuses it: pair 0 stays unrecorded),
+ *                   k_enc_v, k_enc_heads, VWv GEMM, x_g GEMM;
  *   lstm/atten/screen/rescore_events: 2*T events, launch i = step i.  screen = k_vscreen2 /
  *                   k_vscreen (k_vocab under AA_DECODE_EXACT_VOCAB), rescore = k_vrescore (unused
  *                   under AA_DECODE_EXACT_VOCAB; by default only pair T-1 is recorded: the rescoring
