@@ -454,12 +454,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #ifndef AA_ENC4_NW
 #define AA_ENC4_NW 16
 #endif
-#ifndef AA_ENC4_WDB
-#define AA_ENC4_WDB 0
-#endif
-// WDB: the W fragments of stage s + 1 are loaded at the START of stage s into a second register set
-// (a whole stage of MFMAs to land), instead of after each column pair's last MFMA of stage s.
-template <int NCB, int NW = 8, bool WDB = false>
+template <int NCB, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ feats, int B, int C,
                                                 const bf16x8* __restrict__ W4, const float* __restrict__ bias,
                                                 float* __restrict__ V, float* __restrict__ a_g) {
@@ -490,7 +485,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   const int fo = (lane & 15) * E4_LD + 8 * (lane >> 4);
   const bf16x8* wsrc = W4 + (size_t)(wave * NCB) * KC * 3 * 64 + lane;  // block nb = wave NCB + c
   float ra[8];
-  bf16x8 wv0[NCB][3], wv1[WDB ? NCB : 1][3];
+  bf16x8 wv[NCB][3];
   floatx4 acc[E4_RB][NCB];
 #pragma unroll
   for (int rb = 0; rb < E4_RB; ++rb)
@@ -502,7 +497,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
 #pragma unroll
     for (int i = 0; i < 8; ++i) ra[i] = AA_FEAT_LOAD(src + i * P);
   };
-  auto gload_w = [&](int s, int c, bf16x8 (&wv)[NCB][3]) {
+  auto gload_w = [&](int s, int c) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) wv[c][q] = wsrc[((size_t)c * KC * 3 + (size_t)s * 3 + q) * 64];
   };
@@ -525,36 +520,18 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
   };
 
   const int ns = KC;
-  if constexpr (WDB) {
-    // prologue in the loop's steady-state load order (A of the next stage, then this stage's W
-    // youngest), so the waits at the loop head can count instead of draining
-    if (stg) {
-      gload_a(0);
-      lstore_a(0);
-      gload_a(ns > 1 ? 1 : 0);
-    }
+  if (stg) gload_a(0);
 #pragma unroll
-    for (int c = 0; c < NCB; ++c) gload_w(0, c, wv0);
-  } else {
-    if (stg) gload_a(0);
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) gload_w(0, c, wv0);
-    if (stg) lstore_a(0);
-    if (stg) gload_a(ns > 1 ? 1 : 0);
-  }
+  for (int c = 0; c < NCB; ++c) gload_w(0, c);
+  if (stg) lstore_a(0);
+  if (stg) gload_a(ns > 1 ? 1 : 0);
   __syncthreads();
-  // one 32-channel stage; wv: this stage's W fragments, wn: the next stage's (WDB) -- the stage loop
-  // below runs stages in pairs with the two register sets swapped, so both stay statically indexed
-  auto stage = [&](int s, bf16x8 (&wv)[NCB][3], bf16x8 (&wn)[NCB][3]) {
+  for (int s = 0; s < ns; ++s) {
     const int buf = s & 1, s1 = s + 1 < ns ? s + 1 : ns - 1, s2 = s + 2 < ns ? s + 2 : ns - 1;
     // A of stage s+1 (in ra) into the other buffer: its last readers (stage s-1) passed the barrier
     if (stg) {
       lstore_a(buf ^ 1);
       gload_a(s2);
-    }
-    if constexpr (WDB) {
-#pragma unroll
-      for (int c = 0; c < NCB; ++c) gload_w(s1, c, wn);
     }
     __builtin_amdgcn_sched_barrier(0);
     const __bf16* Ab = &As[buf][0][fo];
@@ -586,10 +563,8 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
           acc[rb][c1] = y;
         }
       }
-      if constexpr (!WDB) {
-        gload_w(s1, 2 * cp, wv);
-        gload_w(s1, 2 * cp + 1, wv);
-      }
+      gload_w(s1, 2 * cp);
+      gload_w(s1, 2 * cp + 1);
       // re-read the A fragments for the next pair instead of keeping all 21 live (VGPR budget)
       asm volatile("" ::: "memory");
     }
@@ -608,16 +583,6 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
     }
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
-  };
-  if constexpr (WDB) {
-    int s = 0;
-    for (; s + 1 < ns; s += 2) {
-      stage(s, wv0, wv1);
-      stage(s + 1, wv1, wv0);
-    }
-    if (s < ns) stage(s, wv0, wv1);
-  } else {
-    for (int s = 0; s < ns; ++s) stage(s, wv0, wv0);
   }
   // a_g of the workgroup's images (the last workgroup of an odd batch holds one)
   for (int i = t; i < 2 * C; i += NT) {
@@ -2828,10 +2793,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     // k_enc_v4 computes V and a_g in one pass over the feature map; the a_g branch (heads, x_g)
     // then runs on aux beside the VWv GEMM.  (Trace: the fused avg-pool is a zero-length pair.)
     const int nwg = (B * P + E4_ROWS - 1) / E4_ROWS;
-    if (H == 512 && AA_ENC4_WDB)
-      AA_TLAUNCH(ev, 2, (k_enc_v4<4, 8, true>), dim3(nwg), dim3(512), 0, s, feats, B, C, (const bf16x8*)p.enc_w4,
-                 (const float*)p.enc_a_b, V, a_g);
-    else if (H == 512)
+    if (H == 512)
       AA_TLAUNCH(ev, 2, (k_enc_v4<32 / AA_ENC4_NW, AA_ENC4_NW>), dim3(nwg), dim3(64 * AA_ENC4_NW), 0, s, feats, B, C,
                  (const bf16x8*)p.enc_w4, (const float*)p.enc_a_b, V, a_g);
     else
