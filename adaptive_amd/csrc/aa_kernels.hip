@@ -666,7 +666,8 @@ template <int NB, int NWV, int MODE>
 __global__ __launch_bounds__(64 * NWV) void k_gemm3(const float* __restrict__ A, int M, int K, int N,
                                                     const bf16x8* __restrict__ W4, const float* __restrict__ bias,
                                                     float* __restrict__ out0, int ldo, float* __restrict__ h0,
-                                                    float* __restrict__ c0, int E, int H) {
+                                                    float* __restrict__ c0, int E, int H,
+                                                    bf16x8* __restrict__ hsp = nullptr) {
   constexpr int BN = 16 * NB, TP = BN + 4;  // tile columns, LDS row pitch of a partial tile (floats)
   __shared__ __attribute__((aligned(16))) float Pt[NWV][32 * TP];
   const int KC = K / 32, NTn = (N + BN - 1) / BN;
@@ -757,8 +758,22 @@ __global__ __launch_bounds__(64 * NWV) void k_gemm3(const float* __restrict__ A,
     } else {
       const float x = ps[0] + bias[col];
       if (col < E) out0[(int64_t)row * E + col] = reluf_(x);
-      else if (col < E + H) h0[(int64_t)row * H + (col - E)] = tanhf(x);
-      else c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
+      else if (col < E + H) {
+        const float hv = tanhf(x);
+        const int k = col - E;
+        h0[(int64_t)row * H + k] = hv;
+        if (hsp) {  // k_split_rows's fragments of h0 (the first step's GEMM operand), element by element
+          __bf16 x0, x1, x2;
+          split3(hv, x0, x1, x2);
+          __bf16* o = reinterpret_cast<__bf16*>(hsp + ((size_t)((row >> 5) * (H / 16) + (k >> 4)) * 3) * 64 +
+                                                (row & 31) + 32 * ((k >> 3) & 1)) + (k & 7);
+          o[0] = x0;
+          o[64 * 8] = x1;
+          o[128 * 8] = x2;
+        }
+      } else {
+        c0[(int64_t)row * H + (col - E - H)] = tanhf(x);
+      }
     }
   }
 }
@@ -2749,9 +2764,18 @@ static bool gemm3_ok(int32_t flags, int K) {
 }
 // hsp0 != nullptr (greedy decode): h0 split into the 3-plane fragments k_lstm reads, on `s` after the
 // VWv GEMM, waiting for the heads only (the aux stream's x_g GEMM is still running: off the critical path)
+// init: the greedy decode's k_decode_init (the [T][B] key clear), launched on the aux stream beside
+// k_enc_v4 when there is one (it is needed only from step 1 on), else first on `s`
+struct DecodeInit {
+  int64_t* tok0;
+  int B;
+  uint64_t* keys;
+  int n;
+};
 static int encoder_launch(const Layout& L, const MP& p, const float* feats, int B, float* a_g, float* V, float* v_g,
                           float* h0, float* c0, float* VWv, float* xg, aa_event_t* ev, int32_t flags,
-                          hipStream_t s, hipStream_t aux = nullptr, bf16x8* hsp0 = nullptr) {
+                          hipStream_t s, hipStream_t aux = nullptr, bf16x8* hsp0 = nullptr,
+                          const DecodeInit* init = nullptr) {
   const int C = L.C, H = L.H, E = L.E;
   const int64_t nch = (int64_t)B * C;
   hipEvent_t fork = nullptr, join = nullptr, heads_done = nullptr;
@@ -2764,6 +2788,13 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     AA_TRY(hipStreamWaitEvent(aux, fork, 0));
     sa = aux;
   }
+  if (init) {
+    const int nblk = init->n / 256 + 1;
+    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, sa, init->tok0, init->B,
+                       (int64_t)1, init->keys, init->n);
+  }
+  // the heads kernel also writes h0's bf16x3 fragments for the first step (no k_split_rows launch)
+  const bool heads_split = hsp0 && !(flags & AA_DECODE_FP32_ENCODER || C % 256) && (E + 2 * H) % 80 == 0 && C % 512 == 0;
   auto heads_xg = [&](hipStream_t st) {
     const int NH = E + 2 * H;
     if (flags & AA_DECODE_FP32_ENCODER || C % 256) {
@@ -2772,16 +2803,18 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
                  v_g, h0, c0);
     } else if (NH % 80 == 0 && C % 512 == 0) {
       AA_TLAUNCH(ev, 4, (k_gemm3<5, 8, MODE_HEADS>), dim3(((B + 31) / 32) * (NH / 80)), dim3(512), 0, st,
-                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H);
+                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H,
+                 heads_split ? hsp0 : (bf16x8*)nullptr);
     } else {
       AA_TLAUNCH(ev, 4, (k_gemm3<4, 4, MODE_HEADS>), dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st,
-                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H);
+                 (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H,
+                 (bf16x8*)nullptr);
     }
     if (heads_done) (void)hipEventRecord(heads_done, st);
     if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0) {
       AA_TLAUNCH(ev, 8, (k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st,
                  (const float*)v_g, B, E, L.N5, (const bf16x8*)p.wvg4, (const float*)p.bias5, xg, L.N5, (float*)nullptr,
-                 (float*)nullptr, 0, 0);
+                 (float*)nullptr, 0, 0, (bf16x8*)nullptr);
     } else if (xg) {
       rec(ev, 8, st);
       gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
@@ -2822,13 +2855,14 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
   }
   if (VWv && gemm3_ok(flags, H)) {
     AA_TLAUNCH(ev, 6, (k_gemm3<4, 4, MODE_PLAIN>), dim3((B * P + 31) / 32), dim3(256), 0, s, (const float*)V, B * P, H,
-               PP, (const bf16x8*)p.wv4, (const float*)nullptr, VWv, PP, (float*)nullptr, (float*)nullptr, 0, 0);
+               PP, (const bf16x8*)p.wv4, (const float*)nullptr, VWv, PP, (float*)nullptr, (float*)nullptr, 0, 0,
+               (bf16x8*)nullptr);
   } else if (VWv) {
     rec(ev, 6, s);
     gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);
     rec(ev, 7, s);
   }
-  if (hsp0) {
+  if (hsp0 && !heads_split) {
     if (heads_done) AA_TRY(hipStreamWaitEvent(s, heads_done, 0));
     hipLaunchKernelGGL(k_split_rows, dim3((unsigned)(((int64_t)B * (H / 8) + 255) / 256)), dim3(256), 0, s, h0, B, H,
                        hsp0);
@@ -3149,16 +3183,13 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   DecodeWS w = carve_decode(static_cast<char*>(workspace), L, B, T, &need);
   if (workspace_bytes < need) return AA_ERR_BUFFER;
   const MP p = resolve(m, L);
-  if ((flags & AA_DECODE_EXACT_VOCAB) || ((flags & AA_DECODE_SPLIT_RESCORE) == 0 && T > 1)) {
-    // keys [T][B] cleared: the exact vocab stage accumulates into them by atomicMax (k_vocab); the
-    // fused rescoring publishes them as readiness-tagged granules (a nonzero key = ready, k_lstm<.., RS>).
-    // (The split default writes every key it produces; step 0's k_lstm takes <start> itself.)
-    const int n = T * B, nblk = n / 256 + 1;
-    hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, s, w.tok0, B, (int64_t)1, w.keys,
-                       n);
-  }
+  // keys [T][B] cleared: the exact vocab stage accumulates into them by atomicMax (k_vocab); the
+  // fused rescoring publishes them as readiness-tagged granules (a nonzero key = ready, k_lstm<.., RS>).
+  // (The split default writes every key it produces; step 0's k_lstm takes <start> itself.)
+  const bool clear = (flags & AA_DECODE_EXACT_VOCAB) || ((flags & AA_DECODE_SPLIT_RESCORE) == 0 && T > 1);
+  const DecodeInit init{w.tok0, B, w.keys, T * B};
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
-                      trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0]);
+                      trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0], clear ? &init : nullptr);
   if (rc) return rc;
   return decode_rows(L, p, w, B, T, flags, ids, alpha, beta, trace, s);
 }
