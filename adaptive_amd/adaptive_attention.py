@@ -183,6 +183,8 @@ class DecodePlan:
         d = model.dims
         self.B, self.T = B, T
         self.flags = (_lib.DECODE_EXACT_VOCAB if exact_vocab else 0) | model._decode_flags()
+        if not getattr(model, "decode_aux_stream", False):  # one stream, as sampler (see _decode_into)
+            self.flags |= _lib.DECODE_ONE_STREAM
         self._pack_ref = (model._packed.data_ptr(), model._pack_key)
         self._packed = model._packed  # the graph reads the packed weights: keep them alive
         self.stream = stream
@@ -277,6 +279,8 @@ class Encoder2Decoder(nn.Module):
         # single-process multi-device sampler (device_parallel.py): opt-in -- True (every visible
         # device) or a device list; False / None keep the decode on the images' device
         self.device_parallel = False
+        # the encoder's a_g branch on a second stream (aa_greedy_decode_aux): off, measured slower
+        self.decode_aux_stream = False
         self._replicas = {}  # device index -> device_parallel._Replica
 
     # ---- weights -------------------------------------------------------------------------------
@@ -434,12 +438,16 @@ class Encoder2Decoder(nn.Module):
         ws = self._workspace(lib.aa_decode_workspace_bytes(self._c_dims(), B, T), dev)
         with torch.cuda.device(dev):
             s = stream or torch.cuda.current_stream(dev)
-            # second stream: the encoder's a_g branch (heads, x_g) runs beside the VWv GEMM
-            aux = self._aux_stream(dev)
-            aux.wait_stream(s)  # (the library forks/joins through events too)
+            # one stream by default: the encoder's a_g branch (heads, x_g) beside the VWv GEMM on a
+            # second stream measured slower than the whole decode on one stream (the cross-queue event
+            # waits cost more than the overlap saves: 442 vs 448-457 K captions/s, A/B)
+            aux = None
+            if self.decode_aux_stream:
+                aux = self._aux_stream(dev)
+                aux.wait_stream(s)  # (the library forks/joins through events too)
             rc = lib.aa_greedy_decode_aux(model, images.data_ptr(), B, T, ids.data_ptr(), alpha.data_ptr(),
                                           beta.data_ptr(), _lib.ptr(ws), ws.numel() if ws is not None else 0,
-                                          trace, flags, s.cuda_stream, aux.cuda_stream)
+                                          trace, flags, s.cuda_stream, aux.cuda_stream if aux is not None else None)
         _lib.check(rc, "greedy_decode")
 
     @torch.no_grad()

@@ -454,6 +454,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #ifndef AA_ENC4_NW
 #define AA_ENC4_NW 16
 #endif
+
 template <int NCB, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ feats, int B, int C,
                                                 const bf16x8* __restrict__ W4, const float* __restrict__ bias,
