@@ -25,9 +25,12 @@ in ``pipelined``.  Every mode is timed over >= 5 regions of exactly K steps and 
 reported.  Rank 0 prints ONE JSON line.
 
 Extra fields: ``roofline`` for the dominant kernel (per-launch algorithmic bytes or FLOPs / its
-average duration by timing-only HIP events on its launch stream inside a traced region; for
-``k_atten`` the per-step re-read of V, which SURVEY.md §8d excludes from the algorithmic bytes, is
-priced separately against a MALL read ceiling measured here), ``kernels`` (all per-kernel averages),
+MEDIAN launch duration, from the dispatch's own begin / end timestamps: each traced launch gets a
+hipExtLaunchKernel start / stop event pair on its launch stream -- the timestamps rocprofv3's kernel
+trace reads, so the figure reproduces from the rocprofv3 summary of the same region committed under
+profiles/; for ``k_atten`` the per-step re-read of V, which SURVEY.md §8d excludes from the
+algorithmic bytes, is priced separately against a MALL read ceiling measured here), ``kernels`` (all
+per-kernel medians, means, min / max; ``kernel_sum_ms_per_step`` <= ``ms_per_step``),
 ``path_traffic`` (PMC bytes of every launch of one decode, profiles/traffic.json, over §8d's
 algorithmic bytes), ``hbm_frac_path`` (§8d: bytes(B) per step / step time / 8 TB/s),
 ``fp32_binding`` (§8d's binding figure F x captions/s / 157.3 TF), ``path_roofline`` (every
