@@ -274,6 +274,57 @@ __global__ void k_tgemm_reduce(TG g) {
   *dst = g.accumulate ? *dst + v : v;
 }
 
+// k_tgemm_reduce four columns per thread (16-B partial loads and stores; every element's arithmetic
+// and order exactly k_tgemm_reduce's): for N % 4 == 0 with 16-B aligned C rows, bias and partials
+// (reduce_launch checks).  The element-wise form's 4-B loads ran the largest reduce (dW_m's, 5.2 M
+// elements) at ~2 TB/s.
+__global__ void k_tgemm_reduce4(TG g) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, i = 4 * q;
+  if (i >= (int64_t)g.M * g.N) return;
+  const int m = (int)(i / g.N), n = (int)(i % g.N);
+  const int64_t MN = (int64_t)g.M * g.N;
+  float4 x[SK_MAX];
+#pragma unroll
+  for (int sp = 0; sp < SK_MAX; ++sp)
+    x[sp] = sp < g.splits ? *reinterpret_cast<const float4*>(g.part + sp * MN + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.splits == 1) {
+    v[0] = x[0].x; v[1] = x[0].y; v[2] = x[0].z; v[3] = x[0].w;
+  } else {
+#pragma unroll
+    for (int sp = 0; sp < SK_MAX; ++sp)
+      if (sp < g.splits) {
+        v[0] += x[sp].x; v[1] += x[sp].y; v[2] += x[sp].z; v[3] += x[sp].w;
+      }
+    for (int sp = SK_MAX; sp < g.splits; ++sp) {
+      const float4 y = *reinterpret_cast<const float4*>(g.part + sp * MN + i);
+      v[0] += y.x; v[1] += y.y; v[2] += y.z; v[3] += y.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] + 0.f;
+  }
+  float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + n;
+  const float4 old = g.accumulate ? *reinterpret_cast<const float4*>(dst) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float r[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float t = v[e] + ((g.bias ? g.bias[n + e] : 0.f) + (g.bias2 ? g.bias2[n + e] : 0.f));
+    if (g.act == 1) t = reluf_(t);
+    else if (g.act == 2) t = tanhf(t);
+    r[e] = g.accumulate ? (&old.x)[e] + t : t;
+  }
+  *reinterpret_cast<float4*>(dst) = make_float4(r[0], r[1], r[2], r[3]);
+}
+
+// the split-K reduce of `g`: four columns per thread when the shapes and pointers allow
+static void reduce_launch(const TG& g, hipStream_t s) {
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (g.N % 4 == 0 && g.ldc % 4 == 0 && a16(g.C) && a16(g.part))
+    hipLaunchKernelGGL(k_tgemm_reduce4, dim3((unsigned)(((int64_t)g.M * g.N / 4 + 255) / 256)), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)g.M * g.N + 255) / 256)), dim3(256), 0, s, g);
+}
+
 // k_tgemm's split-K bound (floats of partials): its split counts, and so its fp32 sums, as before
 // the scratch grew for k_bgemm
 constexpr size_t TG_SPLIT_CAP = (size_t)4 << 20;
@@ -326,8 +377,7 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
     hipLaunchKernelGGL(k_tgemm<true>, dim3(tiles * splits), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(k_tgemm<false>, dim3(tiles * splits), dim3(256), 0, s, g);
-  if (splits > 1 && !defer)
-    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, s, g);
+  if (splits > 1 && !defer) reduce_launch(g, s);
   return splits;
 }
 
@@ -587,7 +637,7 @@ static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64
     TG r{};
     r.M = M; r.N = N; r.K = K; r.C = C; r.ldc = ldc; r.crow = crow; r.bias = bias; r.accumulate = accumulate;
     r.splits = splits; r.kper = kper; r.part = gc.split; r.act = act;
-    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0, gc.s, r);
+    reduce_launch(r, gc.s);
   }
 }
 static inline int rup64(int x) { return (x + 63) / 64 * 64; }
@@ -612,7 +662,17 @@ __global__ void k_colsum(const float* __restrict__ X, int M, int N, int64_t ldx,
   if (n >= N) return;
   const int per = (M + CS_CH - 1) / CS_CH, m0 = ch * per, m1 = m0 + per < M ? m0 + per : M;
   float s = 0.f;
-  for (int m = m0; m < m1; ++m) s += X[(int64_t)m * ldx + n];
+  int m = m0;
+  // eight loads in flight, then the eight adds in row order (the same sum, bit for bit, as one row
+  // at a time; a chunk of 98 rows -- the dV bias gradient -- ran ~30 us one dependent load at a time)
+  for (; m + 8 <= m1; m += 8) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = X[(int64_t)(m + j) * ldx + n];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j];
+  }
+  for (; m < m1; ++m) s += X[(int64_t)m * ldx + n];
   part[(int64_t)ch * N + n] = s;
 }
 __global__ void k_colsum_fin(const float* __restrict__ part, int N, float* __restrict__ out) {
