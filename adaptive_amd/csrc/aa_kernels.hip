@@ -1528,14 +1528,6 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
 #ifndef AA_ATTEN_PRIO
 #define AA_ATTEN_PRIO 0
 #endif
-// timing experiments only (wrong results): AA_ATTEN_NOV skips the V loads, AA_ATTEN_NOCHAIN the
-// score / softmax chain
-#ifndef AA_ATTEN_NOV
-#define AA_ATTEN_NOV 0
-#endif
-#ifndef AA_ATTEN_NOCHAIN
-#define AA_ATTEN_NOCHAIN 0
-#endif
 template <int H>
 __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __restrict__ h_new,
                                                 const float* __restrict__ s_new, const float* __restrict__ part,
@@ -1593,7 +1585,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
 #pragma unroll
   for (int i = 0; i < DPT; ++i)
 #pragma unroll
-    for (int kk = 0; kk < VA; ++kk) vv[i][kk] = AA_ATTEN_NOV ? 0.f : vb[(int64_t)kk * H + t + 512 * i];
+    for (int kk = 0; kk < VA; ++kk) vv[i][kk] = vb[(int64_t)kk * H + t + 512 * i];
   if constexpr (VA < P) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VA * DPT) : "memory");
 #pragma unroll
@@ -1635,10 +1627,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   __syncthreads();
   AA_TS(1, 2);
   // 3) softmax (wave 0)
-  if (AA_ATTEN_NOCHAIN) {  // timing experiment only (wrong results): no score chain
-    if (t < PP) sh_alpha[t] = 1.f / 49.f;
-    if (t == 0) sh_beta = 0.5f;
-  } else if (w == 0) {
+  if (w == 0) {
     const float z = lane < P ? zs[lane] : -INFINITY;
     const float zsn = zs[P];
     const float m = wave_max(z);
