@@ -29,10 +29,22 @@ from adaptive_amd.adaptive_attention import synthetic_features
 
 pytestmark = pytest.mark.gpu
 
-# fp32 GEMMs: the tolerances of tests/test_gpu_train.py (same arithmetic, larger batch)
-SCORE_TOL, LOSS_REL, GRAD_REL, GRAD_ENTRY = 1e-4, 1e-5, 1e-3, 1e-2
-# bf16 GEMMs (AA_TRAIN_BF16): the tolerances of test_train_bf16_vs_oracle
-BF16_SCORE_REL, BF16_LOSS_REL, BF16_GRAD_REL = 2e-2, 1e-3, 5e-2
+# Tolerances set from the errors measured at this batch (tools/train_tolerances.py,
+# profiles/r05_train_tolerances.txt), with a 3-7x margin:
+# fp32 GEMMs: scores max abs 4.3e-6, loss rel 1.0e-7, worst gradient rel-Frobenius 4.5e-6 and
+# max-entry/max 5.5e-6 (atten.affine_h)
+SCORE_TOL, LOSS_REL, GRAD_REL, GRAD_ENTRY = 2e-5, 1e-6, 2e-5, 3e-5
+# bf16 GEMMs (AA_TRAIN_BF16): scores rel-Frobenius 3.0e-3, loss rel 2.8e-6, gradients rel-Frobenius
+# 1.5e-2 for encoder.affine_b (its gradient sums all T steps of bf16-rounded products), <= 5.4e-3
+# for every other parameter
+BF16_SCORE_REL, BF16_LOSS_REL = 1e-2, 2e-5
+BF16_GRAD_REL = {"encoder.affine_b.weight": 4.5e-2, "encoder.affine_b.bias": 4.5e-2}
+BF16_GRAD_REL_OTHER = 2e-2
+# after three Adam steps the parameters have drifted apart too: the closure test keeps the
+# previous, looser bounds (not re-measured)
+CLOSURE_LOSS_REL, CLOSURE_NORM_REL = 2e-3, 5e-2
+# Decoder.forward on whole captions (fp32 path, T = 12): not re-measured
+DECODER_SCORE_TOL = 1e-4
 
 
 def _config5_batch(B=128, T=18, seed=0):
@@ -83,7 +95,7 @@ def test_config5_train_step_b128_t18_vs_oracle(config5, gpu_device, bf16):
     for k, p in model.named_parameters():
         g, r = p.grad.detach().cpu().double().numpy(), rgrads[k]
         if bf16:
-            assert np.linalg.norm(g - r) <= BF16_GRAD_REL * max(np.linalg.norm(r), 1e-30), k
+            assert np.linalg.norm(g - r) <= BF16_GRAD_REL.get(k, BF16_GRAD_REL_OTHER) * max(np.linalg.norm(r), 1e-30), k
         else:
             assert np.abs(g - r).max() <= GRAD_ENTRY * max(np.abs(r).max(), 1e-30), k
             assert np.linalg.norm(g - r) <= GRAD_REL * max(np.linalg.norm(r), 1e-30), k
@@ -91,8 +103,8 @@ def test_config5_train_step_b128_t18_vs_oracle(config5, gpu_device, bf16):
 
 def test_config5_adam_clip_closure_vs_oracle(config5, gpu_device):
     """train.py:197-219 three times at config 5 (bf16 GEMMs) beside the same closure on the oracle:
-    per-step loss and the LSTM gradient norm that clip_grad_norm_ reports agree within the bf16
-    tolerances, and the loss goes down."""
+    per-step loss and the LSTM gradient norm that clip_grad_norm_ reports agree within the closure
+    bounds, and the loss goes down."""
     from oracle.adaptive_oracle import TrainOracle
     caps_np, lengths, feats_np, _, _, _ = config5
     oracle = TrainOracle(synth.make_weights(123, bias_noise=0.02))
@@ -116,8 +128,8 @@ def test_config5_adam_clip_closure_vs_oracle(config5, gpu_device):
         rloss.backward()
         rnorm = torch.nn.utils.clip_grad_norm_(o_lstm, 5.0)
         o_opt.step()
-        assert abs(loss.item() - rloss.item()) <= 2 * BF16_LOSS_REL * abs(rloss.item())
-        assert abs(norm.item() - rnorm.item()) <= BF16_GRAD_REL * rnorm.item()
+        assert abs(loss.item() - rloss.item()) <= CLOSURE_LOSS_REL * abs(rloss.item())
+        assert abs(norm.item() - rnorm.item()) <= CLOSURE_NORM_REL * rnorm.item()
         losses.append(loss.item())
     assert losses[2] < losses[1] < losses[0]
     for p in model.parameters():
@@ -220,13 +232,13 @@ def test_decoder_whole_captions_vs_oracle(gpu_device):
     with torch.no_grad():
         osc, oal, obe, (oh, oc) = o.decoder(V.cpu(), v_g.cpu(), caps, (states[0].cpu().contiguous(),
                                                                      states[1].cpu().contiguous()))
-    np.testing.assert_allclose(sc.cpu().numpy(), osc.numpy(), atol=SCORE_TOL, rtol=0)
+    np.testing.assert_allclose(sc.cpu().numpy(), osc.numpy(), atol=DECODER_SCORE_TOL, rtol=0)
     np.testing.assert_allclose(al.cpu().numpy(), oal.numpy(), atol=2e-5, rtol=0)
     np.testing.assert_allclose(be.cpu().numpy(), obe.numpy(), atol=2e-5, rtol=0)
     np.testing.assert_allclose(h.cpu().numpy(), oh.numpy(), atol=1e-5, rtol=0)
     np.testing.assert_allclose(c.cpu().numpy(), oc.numpy(), atol=1e-5, rtol=0)
     # one-token captions still run the sampling step (sentinel h_{t-1} = 0) and agree with T = 1 here
     sc1, al1, be1, _ = m.decoder(V, v_g, caps[:, :1].to(gpu_device), states)
-    np.testing.assert_allclose(sc1.cpu().numpy(), sc[:, :1].cpu().numpy(), atol=SCORE_TOL, rtol=0)
+    np.testing.assert_allclose(sc1.cpu().numpy(), sc[:, :1].cpu().numpy(), atol=DECODER_SCORE_TOL, rtol=0)
     with pytest.raises(IndexError):
         m.decoder(V, v_g, torch.full((B, 3), 10123, dtype=torch.int64, device=gpu_device), states)
