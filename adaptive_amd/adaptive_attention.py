@@ -683,32 +683,39 @@ class Encoder2Decoder(nn.Module):
         HIP backward hands it dL/dA, so CNN fine-tuning, train.py:89, works unchanged)."""
         from torch.nn.utils.rnn import PackedSequence
         images = self._check_images(self.features(images))
-        lengths = [int(n) for n in (lengths.tolist() if torch.is_tensor(lengths) else lengths)]
+        lengths = tuple(int(n) for n in (lengths.tolist() if torch.is_tensor(lengths) else lengths))
         B = images.size(0)
         if captions.dim() != 2 or captions.size(0) != B or len(lengths) != B:
             raise ValueError("captions must be [B, L] and lengths a list of B ints")
-        if any(n < 1 for n in lengths) or any(lengths[i] < lengths[i + 1] for i in range(B - 1)):
-            raise ValueError("lengths must be positive and sorted in decreasing order (pack_padded_sequence)")
+        dev = images.device
+        # per distinct lengths list, validated once and cached: the lengths on the device (a fresh
+        # torch.tensor(..., device=dev) is a pageable host->device copy, which HIP may stage
+        # synchronously: the host then waits before it can queue the rest of the step) and the
+        # PackedSequence batch sizes (an O(B T) Python loop, ~0.1 ms of host time per step at B = 128)
+        cache = self.__dict__.setdefault("_len_dev_cache", {})
+        key = (dev, lengths)
+        hit = cache.get(key)
+        if hit is None:
+            if any(n < 1 for n in lengths) or any(lengths[i] < lengths[i + 1] for i in range(B - 1)):
+                raise ValueError("lengths must be positive and sorted in decreasing order (pack_padded_sequence)")
+            if len(cache) > 64:
+                cache.clear()
+            bs = [0] * lengths[0]
+            for n in lengths:
+                bs[n - 1] += 1
+            for t in range(lengths[0] - 2, -1, -1):  # batch size of step t: rows with length > t
+                bs[t] += bs[t + 1]
+            hit = cache[key] = (torch.tensor(lengths, dtype=torch.int32, device=dev),
+                                torch.tensor(bs, dtype=torch.int64), sum(lengths))
+        len_dev, batch_sizes, N = hit
         T = lengths[0]
         if T > captions.size(1):
             raise ValueError("lengths exceed the caption width")
-        dev = images.device
         caps = captions.to(device=dev, dtype=torch.int64).contiguous()
-        # the lengths on the device, cached per distinct lengths list: a fresh torch.tensor(...,
-        # device=dev) is a pageable host->device copy, which HIP may stage synchronously (the host
-        # then waits before it can queue the rest of the step)
-        cache = self.__dict__.setdefault("_len_dev_cache", {})
-        key = (dev, tuple(lengths))
-        len_dev = cache.get(key)
-        if len_dev is None:
-            if len(cache) > 64:
-                cache.clear()
-            len_dev = cache[key] = torch.tensor(lengths, dtype=torch.int32, device=dev)
-        batch_sizes = torch.tensor([sum(1 for n in lengths if n > t) for t in range(T)], dtype=torch.int64)
         named = dict(self.named_parameters())
         params = [named[k] for _, k in _lib.WEIGHT_FIELDS]
-        data = _TeacherForced.apply(self, images, caps, len_dev, sum(lengths), T, *params)
-        return PackedSequence(data, batch_sizes)
+        data = _TeacherForced.apply(self, images, caps, len_dev, N, T, *params)
+        return PackedSequence(data, batch_sizes.clone())
 
 
 class _TeacherForced(torch.autograd.Function):

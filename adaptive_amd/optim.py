@@ -55,45 +55,62 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = _lib.load()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
-            # validate every parameter of the group first: a rejected tensor must leave no parameter
-            # with a step count for an update that never ran (torch's bias correction would drift)
             live = [p for p in group["params"] if p.grad is not None]
-            for p in live:
-                if p.grad.is_sparse:
-                    raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
-                _require_hip(p, "parameter")
-                _require_hip(p.grad, "gradient")
-                if not (p.is_contiguous() and p.grad.is_contiguous()):
-                    raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
-                if p.grad.shape != p.shape or p.grad.device != p.device:
-                    raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
-            by_step = {}  # tensors that share a step count go in one call
-            for p in live:
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                by_step.setdefault((p.device, float(st["step"].item())), []).append(
-                    (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                     p.numel()))
-            for (dev, step), rows in by_step.items():
-                key = tuple(rows)
-                arr = self._tables.get(key)
-                if arr is None:  # cached per pointer set (the caching allocator hands back the same grads)
-                    arr = (_lib.AdamTensor * len(rows))(*[_lib.AdamTensor(*r) for r in rows])
-                    if len(self._tables) > 16:
-                        self._tables.clear()
-                    self._tables[key] = arr
+            # the validated launch table of this group, reused while the parameters, their gradient
+            # tensors and the state tensors (load_state_dict replaces them) are the ones it was built from (the caching allocator
+            # hands back the same gradient blocks step after step): the per-tensor checks and the
+            # table build then cost nothing per step
+            state = self.state
+            ident = tuple((id(p), id(p.grad), p.data_ptr(), p.grad.data_ptr(),
+                           *(id(x) for x in state[p].values())) if p in state else (id(p),) for p in live)
+            plan = self._tables.get(gi)
+            if plan is None or plan[0] != ident:
+                plan = self._plan(live, ident)
+                if len(self._tables) > 16:
+                    self._tables.clear()
+                self._tables[gi] = plan
+            _, steps, calls = plan
+            # the step counts, as torch.optim.Adam keeps them (CPU float32 tensors), one foreach add
+            torch._foreach_add_(steps, 1.0)
+            for dev, first, arr, n in calls:
+                step = float(steps[first].item())
                 with torch.cuda.device(dev):
-                    rc = lib.aa_adam_step(arr, len(rows), step, group["lr"], beta1, beta2, group["eps"],
+                    rc = lib.aa_adam_step(arr, n, step, group["lr"], beta1, beta2, group["eps"],
                                           group["weight_decay"], _lib.stream_handle())
                 _lib.check(rc, "adam_step")
         return loss
 
+    def _plan(self, live, ident):
+        """Validate the group's live parameters (a rejected tensor leaves no parameter with a step
+        count for an update that never ran: torch's bias correction would drift), create missing
+        state, and group the tensors that share a device and a step count into launch tables."""
+        for p in live:
+            if p.grad.is_sparse:
+                raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
+            _require_hip(p, "parameter")
+            _require_hip(p.grad, "gradient")
+            if not (p.is_contiguous() and p.grad.is_contiguous()):
+                raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
+            if p.grad.shape != p.shape or p.grad.device != p.device:
+                raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
+        steps, by_step = [], {}
+        for i, p in enumerate(live):
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            steps.append(st["step"])
+            by_step.setdefault((p.device, float(st["step"].item())), []).append(
+                (i, (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                     p.numel())))
+        calls = []
+        for (dev, _), rows in by_step.items():
+            arr = (_lib.AdamTensor * len(rows))(*[_lib.AdamTensor(*r) for _, r in rows])
+            calls.append((dev, rows[0][0], arr, len(rows)))
+        return ident, steps, calls
 
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod

@@ -3,6 +3,7 @@
 against torch.optim.Adam (model_factory.py:71), and train.py's closure (train.py:197-219) with both
 against the closure with torch's.  Tolerances: fp32, written per assertion (the two sides round
 exp/log and the reductions in different orders; Adam is in torch's op order)."""
+import copy
 import numpy as np
 import pytest
 import torch
@@ -127,6 +128,36 @@ def test_adam_matches_torch(gpu_device, wd, betas, n_extra):
     oa2 = Adam(pa, lr=1e-3, betas=betas, weight_decay=wd)
     oa2.load_state_dict(orf.state_dict())
     assert float(oa2.state[pa[0]]["step"]) == 4.0
+
+
+def test_adam_reused_plan_and_state_reload(gpu_device):
+    """The cached launch table (gradient tensors kept and overwritten in place, as
+    zero_grad(set_to_none=False) leaves them) gives torch.optim.Adam's steps; load_state_dict then
+    replaces the state tensors mid-run and the next steps use the loaded moments and counts."""
+    from adaptive_amd.optim import Adam
+    pa, pr = _adam_pair(gpu_device, 0)
+    oa = Adam(pa, lr=1e-3)
+    orf = torch.optim.Adam(pr, lr=1e-3)
+    g = torch.Generator(device=gpu_device).manual_seed(2)
+    for a, r in zip(pa, pr):
+        a.grad, r.grad = torch.zeros_like(a), torch.zeros_like(r)
+    for step in range(6):
+        if step == 3:  # both reload the same state: torch's, after three steps
+            sd = orf.state_dict()
+            oa.load_state_dict(copy.deepcopy(sd))  # load_state_dict keeps CPU step tensors: no sharing
+            orf.load_state_dict(copy.deepcopy(sd))
+            for a, r in zip(pa, pr):
+                a.data.copy_(r.data)
+        for a, r in zip(pa, pr):
+            gr = torch.randn(a.shape, device=gpu_device, generator=g)
+            a.grad.copy_(gr)
+            r.grad.copy_(gr)
+        oa.step()
+        orf.step()
+        for a, r in zip(pa, pr):
+            assert float(oa.state[a]["step"]) == float(orf.state[r]["step"]) == step + 1
+            torch.testing.assert_close(a.detach(), r.detach(), rtol=1e-5, atol=1e-7)
+            torch.testing.assert_close(oa.state[a]["exp_avg_sq"], orf.state[r]["exp_avg_sq"], rtol=1e-5, atol=1e-12)
 
 
 def test_train_closure_with_hip_loss_and_adam(gpu_device):
