@@ -668,8 +668,14 @@ __global__ __launch_bounds__(64 * NWV) void k_gemm3(const float* __restrict__ A,
                                                     const bf16x8* __restrict__ W4, const float* __restrict__ bias,
                                                     float* __restrict__ out0, int ldo, float* __restrict__ h0,
                                                     float* __restrict__ c0, int E, int H,
-                                                    bf16x8* __restrict__ hsp = nullptr) {
+                                                    bf16x8* __restrict__ hsp = nullptr, int64_t* __restrict__ tok0 = nullptr,
+                                                    int tok_n = 0, uint64_t* __restrict__ keys = nullptr, int key_n = 0) {
   constexpr int BN = 16 * NB, TP = BN + 4;  // tile columns, LDS row pitch of a partial tile (floats)
+  if (MODE == MODE_HEADS && tok0) {  // k_decode_init's work (one-stream decode): <start> ids, cleared keys
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (int i = i0; i < tok_n; i += stride) tok0[i] = 1;
+    for (int i = i0; i < key_n; i += stride) __hip_atomic_store(keys + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __shared__ __attribute__((aligned(16))) float Pt[NWV][32 * TP];
   const int KC = K / 32, NTn = (N + BN - 1) / BN;
   const int mt = blockIdx.x / NTn, nt = blockIdx.x % NTn;
@@ -2789,13 +2795,17 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     AA_TRY(hipStreamWaitEvent(aux, fork, 0));
     sa = aux;
   }
-  if (init) {
+  // the heads kernel also writes h0's bf16x3 fragments for the first step (no k_split_rows launch)
+  const bool heads_split = hsp0 && !(flags & AA_DECODE_FP32_ENCODER || C % 256) && (E + 2 * H) % 80 == 0 && C % 512 == 0;
+  // on one stream the heads launch (k_gemm3<5, 8, MODE_HEADS>) also does k_decode_init's stores: one
+  // launch fewer on the encoder phase's chain (the ids / keys are first read by step 0 / step 1)
+  const bool init_in_heads = init && sa == s && !(flags & AA_DECODE_FP32_ENCODER || C % 256) &&
+                             (E + 2 * H) % 80 == 0 && C % 512 == 0;
+  if (init && !init_in_heads) {
     const int nblk = init->n / 256 + 1;
     hipLaunchKernelGGL(k_decode_init, dim3(nblk < 1024 ? nblk : 1024), dim3(256), 0, sa, init->tok0, init->B,
                        (int64_t)1, init->keys, init->n);
   }
-  // the heads kernel also writes h0's bf16x3 fragments for the first step (no k_split_rows launch)
-  const bool heads_split = hsp0 && !(flags & AA_DECODE_FP32_ENCODER || C % 256) && (E + 2 * H) % 80 == 0 && C % 512 == 0;
   auto heads_xg = [&](hipStream_t st) {
     const int NH = E + 2 * H;
     if (flags & AA_DECODE_FP32_ENCODER || C % 256) {
@@ -2805,17 +2815,19 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
     } else if (NH % 80 == 0 && C % 512 == 0) {
       AA_TLAUNCH(ev, 4, (k_gemm3<5, 8, MODE_HEADS>), dim3(((B + 31) / 32) * (NH / 80)), dim3(512), 0, st,
                  (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H,
-                 heads_split ? hsp0 : (bf16x8*)nullptr);
+                 heads_split ? hsp0 : (bf16x8*)nullptr, init_in_heads ? init->tok0 : (int64_t*)nullptr,
+                 init_in_heads ? init->B : 0, init_in_heads ? init->keys : (uint64_t*)nullptr,
+                 init_in_heads ? init->n : 0);
     } else {
       AA_TLAUNCH(ev, 4, (k_gemm3<4, 4, MODE_HEADS>), dim3(((B + 31) / 32) * ((NH + 63) / 64)), dim3(256), 0, st,
                  (const float*)a_g, B, C, NH, (const bf16x8*)p.heads_w4, (const float*)p.heads_b, v_g, 0, h0, c0, E, H,
-                 (bf16x8*)nullptr);
+                 (bf16x8*)nullptr, (int64_t*)nullptr, 0, (uint64_t*)nullptr, 0);
     }
     if (heads_done) (void)hipEventRecord(heads_done, st);
     if (xg && gemm3_ok(flags, E) && L.N5 % 80 == 0) {
       AA_TLAUNCH(ev, 8, (k_gemm3<5, 4, MODE_PLAIN>), dim3(((B + 31) / 32) * (L.N5 / 80)), dim3(256), 0, st,
                  (const float*)v_g, B, E, L.N5, (const bf16x8*)p.wvg4, (const float*)p.bias5, xg, L.N5, (float*)nullptr,
-                 (float*)nullptr, 0, 0, (bf16x8*)nullptr);
+                 (float*)nullptr, 0, 0, (bf16x8*)nullptr, (int64_t*)nullptr, 0, (uint64_t*)nullptr, 0);
     } else if (xg) {
       rec(ev, 8, st);
       gemm_bias(v_g, E, B, p.wvg, E, L.N5, E, p.bias5, xg, L.N5, st);
@@ -2857,7 +2869,7 @@ static int encoder_launch(const Layout& L, const MP& p, const float* feats, int 
   if (VWv && gemm3_ok(flags, H)) {
     AA_TLAUNCH(ev, 6, (k_gemm3<4, 4, MODE_PLAIN>), dim3((B * P + 31) / 32), dim3(256), 0, s, (const float*)V, B * P, H,
                PP, (const bf16x8*)p.wv4, (const float*)nullptr, VWv, PP, (float*)nullptr, (float*)nullptr, 0, 0,
-               (bf16x8*)nullptr);
+               (bf16x8*)nullptr, (int64_t*)nullptr, 0, (uint64_t*)nullptr, 0);
   } else if (VWv) {
     rec(ev, 6, s);
     gemm_bias(V, H, B * P, p.wv, H, PP, H, nullptr, VWv, PP, s);

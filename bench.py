@@ -222,9 +222,11 @@ def path_ideal_seconds(B: int, T: int, Vp: int = 10240, v_restream: bool = True)
     return {"total": sum(parts.values()), "parts": parts}
 
 
-# rocprof names of the kernels one decode launches, with launches per decode (profiles/traffic.json)
+# rocprof names of the kernels one default decode launches, with launches per decode
+# (profiles/traffic.json): the heads launch (a k_gemm3) also writes step 0's h fragments and does the
+# id / key initialisation, so k_split_rows and k_decode_init do not run
 def path_launches(T: int) -> dict:
-    return {"k_enc_v4": 1, "k_gemm3": 3, "k_split_rows": 1, "k_decode_init": 1,
+    return {"k_enc_v4": 1, "k_gemm3": 3,
             "k_lstm": T, "k_atten5": T, "k_vscreen2": T, "k_vrescore": 1}  # steps 0..T-2 rescored inside k_lstm
 
 
