@@ -696,15 +696,9 @@ class Encoder2Decoder(nn.Module):
         key = (dev, lengths)
         hit = cache.get(key)
         if hit is None:
-            if any(n < 1 for n in lengths) or any(lengths[i] < lengths[i + 1] for i in range(B - 1)):
-                raise ValueError("lengths must be positive and sorted in decreasing order (pack_padded_sequence)")
+            bs = packed_batch_sizes(lengths)
             if len(cache) > 64:
                 cache.clear()
-            bs = [0] * lengths[0]
-            for n in lengths:
-                bs[n - 1] += 1
-            for t in range(lengths[0] - 2, -1, -1):  # batch size of step t: rows with length > t
-                bs[t] += bs[t + 1]
             hit = cache[key] = (torch.tensor(lengths, dtype=torch.int32, device=dev),
                                 torch.tensor(bs, dtype=torch.int64), sum(lengths))
         len_dev, batch_sizes, N = hit
@@ -716,6 +710,21 @@ class Encoder2Decoder(nn.Module):
         params = [named[k] for _, k in _lib.WEIGHT_FIELDS]
         data = _TeacherForced.apply(self, images, caps, len_dev, N, T, *params)
         return PackedSequence(data, batch_sizes.clone())
+
+
+def packed_batch_sizes(lengths) -> list:
+    """pack_padded_sequence's ``batch_sizes`` for sorted ``lengths`` (step t: the rows longer than t),
+    in O(B + T); raises ValueError, as the reference's packing would, for lengths that are not
+    positive and sorted in decreasing order."""
+    B = len(lengths)
+    if B == 0 or any(n < 1 for n in lengths) or any(lengths[i] < lengths[i + 1] for i in range(B - 1)):
+        raise ValueError("lengths must be positive and sorted in decreasing order (pack_padded_sequence)")
+    bs = [0] * lengths[0]
+    for n in lengths:
+        bs[n - 1] += 1
+    for t in range(lengths[0] - 2, -1, -1):
+        bs[t] += bs[t + 1]
+    return bs
 
 
 class _TeacherForced(torch.autograd.Function):
