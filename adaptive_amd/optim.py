@@ -58,10 +58,12 @@ class Adam(torch.optim.Optimizer):
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
             live = [p for p in group["params"] if p.grad is not None]
+            if not live:
+                continue
             # the validated launch table of this group, reused while the parameters, their gradient
-            # tensors and the state tensors (load_state_dict replaces them) are the ones it was built from (the caching allocator
-            # hands back the same gradient blocks step after step): the per-tensor checks and the
-            # table build then cost nothing per step
+            # tensors and the state tensors (load_state_dict replaces them) are the ones it was built
+            # from (the caching allocator hands back the same gradient blocks step after step): the
+            # per-tensor checks and the table build then cost nothing per step
             state = self.state
             ident = tuple((id(p), id(p.grad), p.data_ptr(), p.grad.data_ptr(),
                            *(id(x) for x in state[p].values())) if p in state else (id(p),) for p in live)
