@@ -1129,9 +1129,6 @@ __device__ __forceinline__ uint64_t rescore_row(int b, bool write, int t, int V,
                                                 const float* __restrict__ bias, uint64_t* __restrict__ keys,
                                                 int64_t* __restrict__ ids, int T, int t_step, float* scr);
 constexpr uint64_t RS_WAIT_TICKS = 5000;  // 50 us of the 100 MHz constant clock
-#ifndef AA_RS_PRIO
-#define AA_RS_PRIO 0
-#endif
 // ring iterations (of H / 32) at which k_lstm<.., RS> DMAs the tile's keys and gathers the table rows
 #ifndef LS_RS_JK
 #define LS_RS_JK 10
@@ -1165,9 +1162,6 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
     static_assert(TS + 2 * RsScratch<H>::FLOATS <= RING_FLOATS, "two rescoring scratch areas beside the tile");
     if (bid < ra.NR) {  // rescoring role (uniform per workgroup): rows 2 bid + (t >> 8)
       AA_TS(4, 0);
-#if AA_RS_PRIO
-      __builtin_amdgcn_s_setprio(AA_RS_PRIO);  // its dependent loads ahead of the GEMM ring's on the CU
-#endif
       const int row = 2 * bid + (int)(threadIdx.x >> 8);
       rescore_row<H, true>(row < B ? row : B - 1, row < B, threadIdx.x & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
                            ra.bias, ra.keys, ra.ids, ra.T, ra.t_step, lds + (threadIdx.x >> 8) * RsScratch<H>::FLOATS);
@@ -1531,9 +1525,6 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
 // flight per CU), the 32 projection partials summed by four groups of 128 threads (8 each, then
 // (g0 + g1) + (g2 + g3)), and each of the 50 scores by 8 lanes (7 terms each, xor-butterfly
 // combine).  Same outputs as k_atten; rounding of the projections / scores differs (fixed orders).
-#ifndef AA_ATTEN_PRIO
-#define AA_ATTEN_PRIO 0
-#endif
 template <int H>
 __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __restrict__ h_new,
                                                 const float* __restrict__ s_new, const float* __restrict__ part,
@@ -1550,11 +1541,6 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   __shared__ float sh_beta;
   __shared__ float sh_norm[16];
   AA_TS(1, 0);
-#if AA_ATTEN_PRIO
-  // the small loads at a raised wave priority, V at the normal one: the CU issues every wave's small
-  // loads before any wave's V stream
-  __builtin_amdgcn_s_setprio(AA_ATTEN_PRIO);
-#endif
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
@@ -1584,10 +1570,6 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
 #define AA_ATTEN_VA P
 #endif
   constexpr int VA = AA_ATTEN_VA < P ? AA_ATTEN_VA : P;
-#if AA_ATTEN_PRIO
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_setprio(0);
-#endif
 #pragma unroll
   for (int i = 0; i < DPT; ++i)
 #pragma unroll
