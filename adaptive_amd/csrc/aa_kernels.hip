@@ -33,6 +33,36 @@
 
 namespace aa {
 
+// Write-through stores (agent-scope relaxed atomic stores = `global_store_* sc1`): the line leaves
+// for memory at once instead of sitting dirty in this XCD's L2 until the kernel-end writeback, which
+// the next launch waits for (MI355X_MICROARCH.md, boundary: + dirty bytes / 6 TB/s).  AA_WT selects
+// which kernel outputs take them: 1 = k_lstm's attention-projection partials, 2 = + k_lstm's h / c /
+// s / split-h, 3 = + k_atten5's u / bf16 u / norms and k_vscreen2's summaries, 4 = + k_enc_v4's V.
+#ifndef AA_WT
+#define AA_WT 2
+#endif
+struct U64x2 {
+  uint64_t a, b;
+};
+template <int LVL, class T>
+__device__ __forceinline__ void st_wt(T* p, const T& v) {
+  if constexpr (AA_WT < LVL) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 4) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 8) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    static_assert(sizeof(T) == 16, "4-, 8- or 16-byte stores");
+    const U64x2 w = __builtin_bit_cast(U64x2, v);
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, w.a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, w.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
 
 // Vocab-screen error bound.  For one logit, the fp32 path (k_vocab / k_vrescore) computes
@@ -45,10 +75,10 @@ constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
 // 4e-6 ||u|| ||w||).  ||du|| comes from the attention kernel that rounds u (the exact differences,
 // Sterbenz), ||dw_n|| from the pack; ||bf16(w)|| <= (1 + 2^-8) ||w||.  The screen applies one bound
 // per (row, 32-column granule g):
-//   E = SC_BF (||du|| W_g + ||u|| D_g) + SC_ACC ||u|| W_g + EPS_ABS (||u|| W_g + B_g),
+//   E = SC_BF (||du|| W_g + ||u|| D_g) + SC_ACC(H) ||u|| W_g + EPS_ABS (||u|| W_g + B_g),
 //   W_g = max_{n in g} ||w_n||, D_g = max ||dw_n||, B_g = max |b_n|
 // SC_BF = 1.005 >= (1 + 2^-8) with the fp32 norms' own rounding (norms inflated at the source);
-// SC_ACC = 5e-5 >= 3.1e-5 + 4e-6 with slack; the EPS_ABS term bounds 2^-17 |A| >= the
+// SC_ACC(512) = 5e-5 >= 3.1e-5 + 4e-6 with slack (sc_acc below); the EPS_ABS term bounds 2^-17 |A| >= the
 // bias-addition roundings plus the < 32-ulp truncation of the screened values that carries the
 // arg-max in their low bits (|A| <= ||u|| ||w_n|| (1 + 2^-7) + |b_n|).  The rounding errors are
 // about 2^-10 relative on average against the worst case 2^-8 per operand, so E is ~2.5x below the
@@ -56,11 +86,21 @@ constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ull;
 // exact rescoring (tools/screen_candidates.py: mean 7.2 -> 2.5 per row, 32-column expansions 10x
 // rarer).  A column n is a candidate iff A_n + E >= max_m (A_m - E): every column holding the
 // exact-fp32 maximum passes, every rejected column is strictly below it.
-constexpr float SC_BF = 1.005f, SC_ACC = 5e-5f;
+// SC_ACC depends on H: the MFMA chain's gamma_H (1 + 2^-8)^2 plus the rescoring's
+// gamma_{H/8 + 4} (8 chains of H/8, the 3-level tree, the bias) is <= 1.1 (H + H/8 + 8) 2^-24;
+// 5e-5 is kept as the floor, so H <= 512 is unchanged (3.8e-5 at H = 512; 5.7e-5 at 768, 7.6e-5
+// at 1024).
+constexpr float SC_BF = 1.005f;
+constexpr float sc_acc(int H) {
+  const float g = 1.1f * (float)(H + H / 8 + 8) * 0x1p-24f;
+  return g > 5e-5f ? g : 5e-5f;
+}
 constexpr float EPS_ABS = 1e-5f;
 // un = (||u||, ||u - bf16(u)||) of the row, g = (W_g, B_g, D_g, -) of the granule, all inflated at
 // their source over their own fp32 rounding
+template <int H>
 __device__ __forceinline__ float screen_bound(float2 un, float4 g) {
+  constexpr float SC_ACC = sc_acc(H);
   const float uw = un.x * g.x;
   return SC_BF * (un.y * g.x + un.x * g.z) + SC_ACC * uw + EPS_ABS * (uw + g.y);
 }
@@ -616,7 +656,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_v4(const float* __restrict__ fe
     for (int q = t; q < F4; q += NT) {
       const int r = q / (H / 4), c4 = q % (H / 4), tr = rb * 16 + r, row = m0 + tr;
       if (tr < E4_ROWS && row < M)
-        *reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4) = *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4);
+        st_wt<4>(reinterpret_cast<float4*>(V + (int64_t)row * H + 4 * c4), *reinterpret_cast<const float4*>(Vs + r * VSP + 4 * c4));
     }
   }
 }
@@ -906,9 +946,9 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
     Ss[u0 * HP + rr] = sn[0];
     Ss[(u0 + 1) * HP + rr] = sn[1];
     if (m < B) {
-      *reinterpret_cast<float2*>(c_out + (int64_t)m * H + j) = make_float2(cn[0], cn[1]);
-      *reinterpret_cast<float2*>(h_out + (int64_t)m * H + j) = make_float2(hn[0], hn[1]);
-      *reinterpret_cast<float2*>(s_out + (int64_t)m * H + j) = make_float2(sn[0], sn[1]);
+      st_wt<2>(reinterpret_cast<float2*>(c_out + (int64_t)m * H + j), make_float2(cn[0], cn[1]));
+      st_wt<2>(reinterpret_cast<float2*>(h_out + (int64_t)m * H + j), make_float2(hn[0], hn[1]));
+      st_wt<2>(reinterpret_cast<float2*>(s_out + (int64_t)m * H + j), make_float2(sn[0], sn[1]));
       if (hsp_out) {
         // next step's A fragments: k = j.. in chunk nt, lane (m % 32) + 32 * (u0 / 8), elements u0 % 8..
         typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -921,9 +961,9 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
         }
         bf16x8* o = hsp_out + ((size_t)((m >> 5) * KC + nt) * 3) * 64 + (m & 31) + 32 * (u0 >> 3);
         const int e = u0 & 7;
-        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e) = p0;
-        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e) = p1;
-        *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e) = p2;
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e), p0);
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e), p1);
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e), p2);
       }
     }
   }
@@ -948,7 +988,7 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mr = m0 + rb * 32 + acc_row(r, lane);
-        if (mr < B) part[((int64_t)mr * NTn + nt) * PART + jg] = pacc[r];
+        if (mr < B) st_wt<1>(&part[((int64_t)mr * NTn + nt) * PART + jg], pacc[r]);
       }
     }
   }
@@ -1520,6 +1560,127 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   }
 }
 
+// The arithmetic of one attention row once its operands are in registers, shared by k_atten5 and
+// the attention role of the fused launch k_lstm<.., AT> (so the two produce the same bits).  Thread t
+// (512 per row): projection group grp = t >> 7, output jp = t & 127 (pv: its H/64 tile partials, tiles
+// grp, grp + 4, ...); score item k = t >> 3, lane q = t & 7 (vwr / whr: its 7 terms j = q + 8 i);
+// context dimensions t + 512 i (hv, sv; V through vget(i, kk)).  The 32 projection partials are summed
+// by the four groups, then (g0 + g1) + (g2 + g3); each of the 50 scores by 8 lanes, xor-butterfly.
+// LVL: the st_wt level of the u / norm stores.
+struct AttSmem {
+  float red[4][128];
+  float proj[PART];
+  float zs[PP];
+  float alpha[PP];
+  float norm[16];
+  float beta;
+};
+template <int H, int LVL, class VG>
+__device__ __forceinline__ void atten_row_math(int B, int b, const float (&pv)[H / 64], const float (&vwr)[7],
+                                               const float (&whr)[7], const float (&hv)[H / 512],
+                                               const float (&sv)[H / 512], VG&& vget, AttSmem& sm,
+                                               float* __restrict__ alpha_out, int64_t alpha_ld,
+                                               float* __restrict__ beta_out, int64_t beta_ld, float* __restrict__ u_out,
+                                               uint16_t* __restrict__ ub_out, float* __restrict__ unorm,
+                                               bf16x8* __restrict__ ub3_out) {
+  constexpr int DPT = H / 512, NG = H / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int grp = t >> 7, jp = t & 127, k = t >> 3, q = t & 7;
+  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
+  {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) a += pv[i];
+    sm.red[grp][jp] = a;
+  }
+  __syncthreads();
+  AA_TS(1, 1);
+  if (t < 2 * P) sm.proj[t] = (sm.red[0][t] + sm.red[1][t]) + (sm.red[2][t] + sm.red[3][t]);
+  __syncthreads();
+  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+      const float x = (k < P ? vwr[i] : sm.proj[P + j]) + sm.proj[j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
+    }
+    z = z + __shfl_xor(z, 1, 64);
+    z = z + __shfl_xor(z, 2, 64);
+    z = z + __shfl_xor(z, 4, 64);
+    if (q == 0 && k <= P) sm.zs[k] = z;
+  }
+  __syncthreads();
+  AA_TS(1, 2);
+  // 3) softmax (wave 0)
+  if (w == 0) {
+    const float z = lane < P ? sm.zs[lane] : -INFINITY;
+    const float zsn = sm.zs[P];
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float S = wave_sum(e);
+    const float a = e / S;
+    if (lane < P) {
+      sm.alpha[lane] = a;
+      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
+    }
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      const float beta = es / S2;
+      sm.beta = beta;
+      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
+    }
+  }
+  __syncthreads();
+  AA_TS(1, 3);
+  // 4) context + u
+  const float beta = sm.beta;
+  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int d = t + 512 * i;
+    float c = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sm.alpha[kk], vget(i, kk), c);
+    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
+    const float u = chat + hv[i];
+    nsq = __builtin_fmaf(u, u, nsq);
+    st_wt<LVL>(&u_out[(int64_t)b * H + d], u);
+    if (ub_out) {
+      const uint16_t ubv = f2bf(u);
+      ub_out[frag_off(b, d, H)] = ubv;  // (2-byte: plain)
+      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
+      dsq = __builtin_fmaf(du, du, dsq);
+    }
+    if (ub3_out) {
+      __bf16 x0, x1, x2;
+      split3(u, x0, x1, x2);
+      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+      o[0] = x0;
+      o[64 * 8] = x1;
+      o[128 * 8] = x2;
+    }
+  }
+  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
+    nsq = wave_sum(nsq);
+    dsq = wave_sum(dsq);
+    if (lane == 0) sm.norm[w] = nsq, sm.norm[8 + w] = dsq;
+    __syncthreads();
+    if (t == 0) {
+      const float* n = sm.norm;
+      st_wt<LVL>(&unorm[b], sqrtf(((n[0] + n[1]) + (n[2] + n[3])) + ((n[4] + n[5]) + (n[6] + n[7]))) * 1.0001f);
+      st_wt<LVL>(&unorm[B + b],
+                 sqrtf(((n[8] + n[9]) + (n[10] + n[11])) + ((n[12] + n[13]) + (n[14] + n[15]))) * 1.0001f);
+    }
+  }
+  AA_TS(1, 4);
+}
+
 // k_atten with two threads per output dimension's worth of parallelism: 512 threads per row, each
 // owning H/512 dimensions of the context (half the V registers of k_atten<2>, twice the waves in
 // flight per CU), the 32 projection partials summed by four groups of 128 threads (8 each, then
@@ -1534,14 +1695,9 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
                                                 float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
                                                 float* __restrict__ unorm, bf16x8* __restrict__ ub3_out) {
   constexpr int DPT = H / 512, NT16 = H / 16, NG = NT16 / 4;
-  __shared__ float red[4][128];
-  __shared__ float proj[PART];
-  __shared__ float zs[PP];
-  __shared__ float sh_alpha[PP];
-  __shared__ float sh_beta;
-  __shared__ float sh_norm[16];
+  __shared__ AttSmem sm;
   AA_TS(1, 0);
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
   // loads, oldest first in the order they are consumed; clamped addresses, no branches
@@ -1587,99 +1743,8 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
     hv[i] = h_new[(int64_t)b * H + t + 512 * i];
     sv[i] = s_new[(int64_t)b * H + t + 512 * i];
   }
-  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
-  {
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < NG; ++i) a += pv[i];
-    red[grp][jp] = a;
-  }
-  __syncthreads();
-  AA_TS(1, 1);
-  if (t < 2 * P) proj[t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-  __syncthreads();
-  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
-  {
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
-      const float x = (k < P ? vwr[i] : proj[P + j]) + proj[j];
-      z = __builtin_fmaf(whr[i], tanhf(x), z);
-    }
-    z = z + __shfl_xor(z, 1, 64);
-    z = z + __shfl_xor(z, 2, 64);
-    z = z + __shfl_xor(z, 4, 64);
-    if (q == 0 && k <= P) zs[k] = z;
-  }
-  __syncthreads();
-  AA_TS(1, 2);
-  // 3) softmax (wave 0)
-  if (w == 0) {
-    const float z = lane < P ? zs[lane] : -INFINITY;
-    const float zsn = zs[P];
-    const float m = wave_max(z);
-    const float e = lane < P ? expf(z - m) : 0.f;
-    const float S = wave_sum(e);
-    const float a = e / S;
-    if (lane < P) {
-      sh_alpha[lane] = a;
-      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
-    }
-    const float m2 = fmaxf(m, zsn);
-    const float e2 = lane < P ? expf(z - m2) : 0.f;
-    const float es = expf(zsn - m2);
-    const float S2 = wave_sum(e2) + es;
-    if (lane == 0) {
-      const float beta = es / S2;
-      sh_beta = beta;
-      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
-    }
-  }
-  __syncthreads();
-  AA_TS(1, 3);
-  // 4) context + u
-  const float beta = sh_beta;
-  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
-#pragma unroll
-  for (int i = 0; i < DPT; ++i) {
-    const int d = t + 512 * i;
-    float c = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sh_alpha[kk], vv[i][kk], c);
-    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
-    const float u = chat + hv[i];
-    nsq = __builtin_fmaf(u, u, nsq);
-    u_out[(int64_t)b * H + d] = u;
-    if (ub_out) {
-      const uint16_t ubv = f2bf(u);
-      ub_out[frag_off(b, d, H)] = ubv;
-      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
-      dsq = __builtin_fmaf(du, du, dsq);
-    }
-    if (ub3_out) {
-      __bf16 x0, x1, x2;
-      split3(u, x0, x1, x2);
-      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
-                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
-      o[0] = x0;
-      o[64 * 8] = x1;
-      o[128 * 8] = x2;
-    }
-  }
-  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
-    nsq = wave_sum(nsq);
-    dsq = wave_sum(dsq);
-    if (lane == 0) sh_norm[w] = nsq, sh_norm[8 + w] = dsq;
-    __syncthreads();
-    if (t == 0) {
-      unorm[b] = sqrtf(((sh_norm[0] + sh_norm[1]) + (sh_norm[2] + sh_norm[3])) +
-                       ((sh_norm[4] + sh_norm[5]) + (sh_norm[6] + sh_norm[7]))) * 1.0001f;
-      unorm[B + b] = sqrtf(((sh_norm[8] + sh_norm[9]) + (sh_norm[10] + sh_norm[11])) +
-                           ((sh_norm[12] + sh_norm[13]) + (sh_norm[14] + sh_norm[15]))) * 1.0001f;
-    }
-  }
-  AA_TS(1, 4);
+  atten_row_math<H, 3>(B, b, pv, vwr, whr, hv, sv, [&](int i, int kk) { return vv[i][kk]; }, sm, alpha_out, alpha_ld,
+                       beta_out, beta_ld, u_out, ub_out, unorm, ub3_out);
 }
 
 // k_atten5 for beam search: one workgroup per IMAGE runs the KB rows (beams) of that image, so the
@@ -1700,7 +1765,7 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
   __shared__ float zs[KB][PP];
   __shared__ float sh_alpha[KB][PP];
   __shared__ float sh_beta[KB];
-  __shared__ float sh_norm[KB][8];
+  __shared__ float sh_norm[KB][16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int img = blockIdx.x, r0 = img * KB;
   const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
@@ -1794,7 +1859,7 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
   for (int r = 0; r < KB; ++r) {
     const int b = r0 + r;
     const float beta = sh_beta[r];
-    float nsq = 0.f;
+    float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2, as k_atten5 (the screen's bound)
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int d = t + 512 * i;
@@ -1805,7 +1870,12 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
       const float u = chat + hv[r][i];
       nsq = __builtin_fmaf(u, u, nsq);
       u_out[(int64_t)b * H + d] = u;
-      if (ub_out) ub_out[frag_off(b, d, H)] = f2bf(u);
+      if (ub_out) {
+        const uint16_t ubv = f2bf(u);
+        ub_out[frag_off(b, d, H)] = ubv;
+        const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
+        dsq = __builtin_fmaf(du, du, dsq);
+      }
       if (ub3_out) {
         __bf16 x0, x1, x2;
         split3(u, x0, x1, x2);
@@ -1818,14 +1888,18 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
     }
     if (unorm) {
       nsq = wave_sum(nsq);
-      if (lane == 0) sh_norm[r][w] = nsq;
+      dsq = wave_sum(dsq);
+      if (lane == 0) sh_norm[r][w] = nsq, sh_norm[r][8 + w] = dsq;
     }
   }
-  if (unorm) {
+  if (unorm) {  // [2][B] as k_atten5 writes it (B = the launch's rows: one workgroup per KB rows)
     __syncthreads();
-    if (t < KB)
-      unorm[r0 + t] = sqrtf(((sh_norm[t][0] + sh_norm[t][1]) + (sh_norm[t][2] + sh_norm[t][3])) +
-                            ((sh_norm[t][4] + sh_norm[t][5]) + (sh_norm[t][6] + sh_norm[t][7]))) * 1.00001f;
+    const int B = gridDim.x * KB;
+    if (t < KB) {
+      const float* n = sh_norm[t];
+      unorm[r0 + t] = sqrtf(((n[0] + n[1]) + (n[2] + n[3])) + ((n[4] + n[5]) + (n[6] + n[7]))) * 1.0001f;
+      unorm[B + r0 + t] = sqrtf(((n[8] + n[9]) + (n[10] + n[11])) + ((n[12] + n[13]) + (n[14] + n[15]))) * 1.0001f;
+    }
   }
 }
 
@@ -1992,7 +2066,7 @@ __global__ __launch_bounds__(256, 2) void k_vscreen(int B, int V, int Vp, const 
       if (!(li & 1) && row < B) {
         float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
         if (m1) {
-          const float E = screen_bound(un_s[rl], gsv);
+          const float E = screen_bound<H>(un_s[rl], gsv);
           const float x1 = key_value(m1 & ~31u);
           const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
           o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + c) * VS_TILE + (int)(m1 & 31u)));
@@ -2017,6 +2091,7 @@ constexpr int SC2_STAGE = SC2_NB * SC2_KS * 64;  // bf16x8 per LDS stage (20 KB)
 
 // Per (row, granule) summary of one 32 x 32 block of screened logits in MFMA C layout (rows row0..,
 // columns 32 G..): keys, transposing top-2 butterfly, bound E, one float4 per row (see k_vscreen).
+template <int H>
 __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0, int G, float bv, float4 gsv,
                                                   const float2* __restrict__ un_blk, bool valid, int B, int NTn,
                                                   float4* __restrict__ summ) {
@@ -2042,7 +2117,7 @@ __device__ __forceinline__ void screen_block_summ(const floatx16& blk, int row0,
   if (!(li & 1) && row < B) {
     float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
     if (m1) {
-      const float E = screen_bound(un_blk[rl], gsv);
+      const float E = screen_bound<H>(un_blk[rl], gsv);
       const float x1 = key_value(m1 & ~31u);
       const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
       o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float(G * VS_TILE + (int)(m1 & 31u)));
@@ -2091,7 +2166,7 @@ __device__ __forceinline__ void screen_bfly16_swap(uint32_t (&k1)[16], uint32_t 
   }
 }
 
-template <int NB>
+template <int H, int NB>
 __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], int row0, int G0, const float (&bv)[NB],
                                                    const float4* __restrict__ gsb, const float2* __restrict__ un_blk,
                                                    int c0, int V, int B, int NTn, float4* __restrict__ summ) {
@@ -2128,12 +2203,12 @@ __device__ __forceinline__ void screen_blocks_summ(const floatx16 (&acc)[NB], in
     if (!(li & 1) && row < B) {
       float4 o = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
       if (m1) {
-        const float E = screen_bound(uw0, gsb[b]);
+        const float E = screen_bound<H>(uw0, gsb[b]);
         const float x1 = key_value(m1 & ~31u);
         const float x2 = m2 ? key_value(m2 & ~31u) : -INFINITY;
         o = make_float4(x1 - E, x1 + E, x2 + E, __int_as_float((G0 + b) * VS_TILE + (int)(m1 & 31u)));
       }
-      summ[(int64_t)row * NTn + G0 + b] = o;
+      st_wt<3>(&summ[(int64_t)row * NTn + G0 + b], o);
     }
   }
 }
@@ -2247,13 +2322,13 @@ __global__ __launch_bounds__(256, AA_SCREEN_OCC) void k_vscreen2(int B, int V, i
 #define AA_SCREEN_EPI 1
 #endif
 #if AA_SCREEN_EPI
-  screen_blocks_summ<SC2_NB>(acc, row0, n0 / VS_TILE, bvs, AA_SCREEN_GS_LDS ? gs_s : gs + n0 / VS_TILE,
+  screen_blocks_summ<H, SC2_NB>(acc, row0, n0 / VS_TILE, bvs, AA_SCREEN_GS_LDS ? gs_s : gs + n0 / VS_TILE,
                              un_s + 32 * wave, n0, V, B, NTn, summ);
 #else
 #pragma unroll
   for (int b = 0; b < SC2_NB; ++b) {
     const int G = n0 / VS_TILE + b;
-    screen_block_summ(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
+    screen_block_summ<H>(acc[b], row0, G, bvs[b], gs[G], un_s + 32 * wave, n0 + 32 * b + li < V, B, NTn, summ);
   }
 #endif
   AA_TS(2, 2);

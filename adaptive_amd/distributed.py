@@ -10,6 +10,7 @@ CPU tests.
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, List, Optional, Tuple
 
 import torch
@@ -69,8 +70,10 @@ def pack_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, list]:
             raise ValueError("pack_rows: every tensor needs the same number of rows")
         if t.element_size() % 4:
             raise ValueError(f"pack_rows: {t.dtype} is not a multiple of 32 bits")
-        flat = t.contiguous().view(n, -1)
-        words = flat.view(torch.int32) if flat.numel() else flat.new_empty((n, 0), dtype=torch.int32)
+        # explicit row width: view(0, -1) is ambiguous for torch, and a rank may hold 0 rows when the
+        # batch is smaller than the world (the other ranks would then wait in the all-gather forever)
+        width = math.prod(t.shape[1:]) * t.element_size() // 4
+        words = t.contiguous().reshape(n, -1 if n else 0).view(torch.int32).reshape(n, width)
         cols.append(words)
         spec.append((t.dtype, tuple(t.shape[1:]), words.size(1)))
     return torch.cat(cols, dim=1).contiguous(), spec

@@ -7,6 +7,7 @@ loaded by torch (``libamdhip64.so.7``).
 from __future__ import annotations
 
 import ctypes
+import warnings
 from ctypes import POINTER, c_float, c_int, c_void_p
 
 import torch  # noqa: F401  (loads torch's HIP runtime first)
@@ -168,17 +169,22 @@ def role_stream(device, role: str) -> "torch.cuda.ExternalStream":
 
 HIP_MEMCPY_DEFAULT = 4  # hipMemcpyDefault: direction from the pointers (unified addressing)
 HIP_ERROR_PEER_ACCESS_ALREADY_ENABLED = 704
-_peer_done = set()
+_peer_state = {}  # (a, b) -> peer access enabled (True) or no P2P path (False)
 
 
-def enable_peer_access(a: int, b: int) -> None:
+def enable_peer_access(a: int, b: int) -> bool:
     """Let devices ``a`` and ``b`` read and write each other's memory (hipDeviceEnablePeerAccess in
     both directions; idempotent: "already enabled" counts as success).  Done explicitly before the
     first peer copy of a single-process multi-device decode instead of relying on a side effect of
-    torch's cross-device ``.to()``.  Raises if the pair cannot access each other (no P2P path)."""
+    torch's cross-device ``.to()``.  Returns False (and warns once per pair) when
+    hipDeviceCanAccessPeer reports no P2P path: the decode's ``hipMemcpyAsync(hipMemcpyDefault)``
+    copies then stage through the host -- slower, still correct.  Both outcomes are cached, so the
+    check runs once per pair."""
     a, b = int(a), int(b)
-    if a == b or (a, b) in _peer_done:
-        return
+    if a == b:
+        return True
+    if (a, b) in _peer_state:
+        return _peer_state[(a, b)]
     h = hip()
     h.hipDeviceCanAccessPeer.argtypes = [ctypes.POINTER(c_int), c_int, c_int]
     h.hipDeviceCanAccessPeer.restype = c_int
@@ -188,13 +194,17 @@ def enable_peer_access(a: int, b: int) -> None:
         ok = c_int(0)
         rc = h.hipDeviceCanAccessPeer(ctypes.byref(ok), src, dst)
         if rc != 0 or not ok.value:
-            raise RuntimeError(f"device {src} cannot access device {dst} (hipDeviceCanAccessPeer rc={rc})")
+            warnings.warn(f"adaptive_amd: device {src} cannot access device {dst} directly "
+                          f"(hipDeviceCanAccessPeer rc={rc}); peer copies stage through the host")
+            _peer_state[(a, b)] = _peer_state[(b, a)] = False
+            return False
+    for src, dst in ((a, b), (b, a)):
         with torch.cuda.device(src):
             rc = h.hipDeviceEnablePeerAccess(dst, 0)
         if rc not in (0, HIP_ERROR_PEER_ACCESS_ALREADY_ENABLED):
             raise RuntimeError(f"hipDeviceEnablePeerAccess({src} -> {dst}) failed: {rc}")
-    _peer_done.add((a, b))
-    _peer_done.add((b, a))
+    _peer_state[(a, b)] = _peer_state[(b, a)] = True
+    return True
 
 
 def copy_async(dst: "torch.Tensor", src: "torch.Tensor", stream) -> None:

@@ -312,25 +312,82 @@ def time_region(run, world: int, sync, dev) -> float:
     return el
 
 
+def _comm_device(world: int, dev):
+    """Where a small bookkeeping collective's tensor lives: the rank's GPU for nccl (RCCL), the host
+    for gloo (CPU tests, and the one-GPU gloo rehearsal)."""
+    return dev if world > 1 and dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def rank_topology(world: int, rank: int, local: int, dev) -> dict:
+    """Every rank's (rank, LOCAL_RANK, device index, PCI domain / bus / device id), all-gathered
+    (one small collective outside the timed regions), so the line shows which device each rank ran
+    on and that no two ranks shared one (for ``nccl``, one process per GPU)."""
+    if dev.type == "cuda":
+        pr = torch.cuda.get_device_properties(dev)
+        mine = [rank, local, dev.index, pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id]
+    else:
+        mine = [rank, local, -1, -1, -1, -1]
+    cdev = _comm_device(world, dev)
+    t = torch.tensor(mine, dtype=torch.int64, device=cdev)
+    if world > 1:
+        allt = torch.empty(world * len(mine), dtype=torch.int64, device=cdev)
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(allt, t)
+        else:
+            dist.all_gather(list(allt.chunk(world)), t)
+        rows = allt.view(world, len(mine)).tolist()
+    else:
+        rows = [mine]
+    ranks = [{"rank": r[0], "local_rank": r[1], "device": r[2], "pci": f"{r[3]:04x}:{r[4]:02x}:{r[5]:02x}"}
+             for r in rows]
+    keys = [(r["device"], r["pci"]) for r in ranks]
+    return {"ranks": ranks, "distinct_devices": dev.type == "cuda" and len(set(keys)) == len(keys)}
+
+
+def cross_check(world: int, rank: int, B: int, gathered: torch.Tensor, decode_shard, dev) -> dict:
+    """Rank r recomputes rank (r + 1) % world's shard locally (``decode_shard(peer)`` -> [B, T]) and
+    compares it with those rows of the all-gathered ids: the gather delivered every rank's rows to the
+    right place and the ranks decode identically.  The per-rank results are AND-reduced (all_reduce
+    MIN), so rank 0's line holds every rank's verdict.  Outside the timed regions."""
+    peer = (rank + 1) % world
+    mine = torch.equal(gathered[peer * B:(peer + 1) * B].cpu(), decode_shard(peer).cpu())
+    ok = torch.tensor([1 if mine else 0], dtype=torch.int64, device=_comm_device(world, dev))
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"ok": bool(ok.item()), "peer_of_rank": "(rank + 1) % world",
+            "what": "each rank re-decoded its neighbour's shard locally and compared it with the gathered ids"}
+
+
 def plumbing_main(args, world: int, rank: int) -> None:
     """``--cpu-plumbing``: the N > 1 launch path without a GPU (CPU tests): gloo ranks, the ids
     all-gather of a stand-in [B, T] shard through adaptive_amd.distributed.gather_rows, timed regions
-    with max-over-ranks, one JSON line from rank 0.  Measures nothing about the decode."""
+    with max-over-ranks, the rank topology and the neighbour-shard cross-check of the GPU line, one
+    JSON line from rank 0.  Measures nothing about the decode (the stand-in "decode" is a fixed
+    function of the global row and step)."""
     dist.init_process_group("gloo")
     B, T = args.batch, args.max_len
     dev = torch.device("cpu")
-    ids = torch.arange(rank * B * T, (rank + 1) * B * T, dtype=torch.int64).view(B, T)
+
+    def decode_shard(r):
+        return (torch.arange(r * B, (r + 1) * B, dtype=torch.int64).view(B, 1) * 7919
+                + torch.arange(T, dtype=torch.int64).view(1, T)) % 10123
+
+    ids = decode_shard(rank)
     got = []
 
     def run():
         got.append(gather_rows(ids, world * B))
 
     regions = [time_region(run, world, lambda: None, dev) for _ in range(max(5, args.regions))]
-    ok = all(torch.equal(g, torch.arange(world * B * T, dtype=torch.int64).view(world * B, T)) for g in got)
+    want = torch.cat([decode_shard(r) for r in range(world)])
+    ok = all(torch.equal(g, want) for g in got)
+    topo = rank_topology(world, rank, int(os.environ.get("LOCAL_RANK", "0")), dev)
+    xc = cross_check(world, rank, B, got[-1], decode_shard, dev)
     if rank == 0:
         print(json.dumps({"metric": "plumbing rehearsal (no GPU, no decode)", "value": None, "n_gpus": world,
                           "ranks_seen": dist.get_world_size(), "backend": dist.get_backend(),
-                          "gathered_ok": ok, "regions_s": regions}), flush=True)
+                          "gathered_ok": ok, "rank_devices": topo, "cross_check": xc,
+                          "regions_s": regions}), flush=True)
     dist.destroy_process_group()
 
 
@@ -600,6 +657,17 @@ def main():
             roofline["algorithmic_bytes_per_launch"] = ka["algorithmic_bytes_per_launch"]
             roofline["v_restream"] = atten_v
 
+    # N > 1 evidence outside the timed regions: which device each rank ran on, and the gathered ids
+    # of the canonical batch against a local re-decode of the neighbouring rank's shard
+    topo = rank_topology(world, rank, local, dev) if world > 1 else None
+    xcheck = None
+    if world > 1:
+        gathered = gather_rows(model.sampler(feats, max_len=T)[0], world * B)
+        xcheck = cross_check(world, rank, B, gathered,
+                             lambda r: model.sampler(synthetic_features(B, dev, seed=0, row0=r * B), max_len=T)[0],
+                             dev)
+        del gathered
+
     ideal = path_ideal_seconds(B, T, v_restream=False)
     ideal_exec = path_ideal_seconds(B, T, v_restream=True)
     F = flops_per_caption(T)["total"]
@@ -636,6 +704,8 @@ def main():
                    "headline": "one sampler() call after another on resident batches"},
         "ranks_seen": dist.get_world_size() if world > 1 else 1,
         "backend": (dist.get_backend() if world > 1 else None),
+        "rank_devices": topo,
+        "cross_check": xcheck,
         "regions": {"count": R, "sequential_captions_per_s": [captions / e for e in seq_regions],
                     "pipelined_captions_per_s": [captions / e for e in pipe_regions], "reported": "median"},
         "eval_loop": eval_block,

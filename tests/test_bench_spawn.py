@@ -1,7 +1,8 @@
 """bench.py's N > 1 entry point as the driver runs it (`python bench.py --gpus N`, no torchrun):
 bench.py starts the N ranks itself (torch.distributed.run as a child process) and rank 0 prints
 exactly one JSON line.  On CPU the ranks run the ``--cpu-plumbing`` path (gloo, the ids all-gather
-through adaptive_amd.distributed.gather_rows, max-over-ranks timing) -- no GPU, no decode."""
+through adaptive_amd.distributed.gather_rows, max-over-ranks timing, the rank topology and the
+neighbour-shard cross-check) -- no GPU, no decode.  N = 8 is the node the driver's scaling run uses."""
 import json
 import os
 import subprocess
@@ -12,7 +13,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_spawns_its_own_ranks(n):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
@@ -29,6 +30,12 @@ def test_bench_spawns_its_own_ranks(n):
     assert d["n_gpus"] == n and d["ranks_seen"] == n and d["backend"] == "gloo"
     assert d["gathered_ok"] is True
     assert len(d["regions_s"]) >= 5
+    # what the GPU line carries for N > 1 too: every rank listed once, and every rank's re-decode of its
+    # neighbour's shard equal to the gathered rows (AND over the ranks)
+    ranks = d["rank_devices"]["ranks"]
+    assert sorted(r["rank"] for r in ranks) == list(range(n))
+    assert sorted(r["local_rank"] for r in ranks) == list(range(n))
+    assert d["cross_check"]["ok"] is True
 
 
 def test_bench_refuses_mismatched_world():

@@ -67,21 +67,25 @@ def _worker(rank, world, port, total, T, q):
         calls = []
         real = D._all_gather
         D._all_gather = lambda out, inp, group: (calls.append(tuple(inp.shape)), real(out, inp, group))
+        def decode(x, t):  # an empty shard (total < world) decodes to empty outputs, as the HIP path does
+            if x.size(0) == 0:
+                return (torch.empty(0, t, dtype=torch.int64), torch.empty(0, t, 49), torch.empty(0, t, 1))
+            return m.sampler(x, max_len=t)
         try:
-            ids, alpha, beta = sharded_sampler(lambda x, t: m.sampler(x, max_len=t), feats, total, T,
-                                               gather_attention=True)
+            ids, alpha, beta = sharded_sampler(decode, feats, total, T, gather_attention=True)
         finally:
             D._all_gather = real
         assert len(calls) == 1, calls  # ids, alpha and beta in ONE collective
         x = gather_rows(torch.arange(lo, hi, dtype=torch.int64).view(-1, 1), total)
-        if rank == 0:
-            q.put((ids, alpha, beta, x))
+        if rank == 0:  # by value (numpy): a tensor would travel as a shared-memory fd that this process
+            q.put(tuple(v.numpy() for v in (ids, alpha, beta, x)))  # may close before the parent opens it
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total", [6, 5])
+@pytest.mark.parametrize("total", [6, 5, 1])
 def test_sharded_decode_equals_full_batch(total):
+    """total = 1 < world: rank 1 holds no rows and still joins the one all-gather."""
     world, T = 2, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -89,7 +93,7 @@ def test_sharded_decode_equals_full_batch(total):
              for r in range(world)]
     for p in procs:
         p.start()
-    ids, alpha, beta, x = q.get(timeout=300)
+    ids, alpha, beta, x = (torch.from_numpy(v) for v in q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -103,4 +107,4 @@ def test_sharded_decode_equals_full_batch(total):
     torch.testing.assert_close(beta, r_beta, atol=1e-6, rtol=0)
 
 
-PORTS = {6: _free_port(), 5: _free_port()}
+PORTS = {6: _free_port(), 5: _free_port(), 1: _free_port()}

@@ -194,10 +194,12 @@ def test_decode_plan_replay_equals_sampler(model, gpu_device, exact):
     plan.close()
 
 
-@pytest.mark.parametrize("hidden,B", [(256, 37), (768, 20)])
+@pytest.mark.parametrize("hidden,B", [(256, 37), (768, 20), (1024, 24)])
 def test_other_hidden_sizes_vs_oracle(gpu_device, hidden, B):
-    """The general-dims kernels: hidden 256 (k_vscreen2 tiles, k_enc_v4<2>) and 768 (the 64 x 64
-    screen k_vscreen, the 128 x 128-tile encoder k_enc_v3, k_atten<3>) against the oracle."""
+    """The general-dims kernels: hidden 256 (k_vscreen2 tiles, k_enc_v4<2>), 768 and 1024 (the 64 x 64
+    screen k_vscreen, the 128 x 128-tile encoder k_enc_v3, k_atten<HPT>) against the oracle; the
+    screened ids equal the exact-vocab ids (the screen bound's H-dependent accumulation term,
+    sc_acc(H))."""
     from adaptive_amd import Config, Encoder2Decoder
     from oracle.adaptive_oracle import OracleModel
     cf = Config(adaptive_word_embed_size=256, adaptive_lstm_hidden_size=hidden, vocab_length=3001)
