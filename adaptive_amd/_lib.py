@@ -23,10 +23,6 @@ DECODE_FP32_ENCODER = 2
 DECODE_ONE_STREAM = 512
 DECODE_SPLIT_RESCORE = 1024  # rescoring in its own launch per step (cross-check of the fused default)
 DECODE_RS_SELF = 2048  # test hook: fused launch's LSTM workgroups rescore unpublished rows themselves
-DECODE_SPLIT_ATTEN = 4096  # attention in its own launch per step (cross-check of the fused default, hidden 512)
-DECODE_AT_SELF = 8192  # test hook: each row block's last LSTM workgroup computes every unclaimed attention row
-LAUNCH_RESCORE_IN_LSTM = 1  # aa_decode_launch_structure bits
-LAUNCH_ATTEN_IN_LSTM = 2
 BEAM_FAST = 256
 TRAIN_BF16 = 128
 MAX_BEAM = 8
@@ -100,7 +96,6 @@ SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p]),
     "aa_decode_workspace_bytes": (c_size_t, [POINTER(Dims), c_int32, c_int32]),
-    "aa_decode_launch_structure": (c_int, [POINTER(Dims), c_int32]),
     "aa_greedy_decode": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_size_t, POINTER(Trace), c_int32, c_void_p]),
     "aa_greedy_decode_aux": (c_int, [POINTER(Model), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,

@@ -865,12 +865,7 @@ __global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, 
 // (Atten.affine_g / affine_s, adaptive_attention.py:35,45): part[b][tile][j] = sum_{u in tile}
 // (j < 49 ? h'_u W_g[j][u] : s_u W_s[j-49][u]); k_atten adds the H/16 partials in tile order.
 // ---------------------------------------------------------------------------------------------
-constexpr int PART = 128;  // partial-projection row pitch: W_g h outputs at 0..48, W_s s outputs at 64..112
-// Column of projection output j (0..97: W_g then W_s) in a partial row.  Each half starts on a 256-B
-// boundary, so every store instruction of the tile's projection phase (a 32 x 32 accumulator block:
-// two rows x 32 columns) writes two whole 128-B lines -- write-through stores of partial lines cost
-// the memory side a read-modify-write each.
-__device__ __forceinline__ int part_col(int j) { return j < P ? j : 64 + (j - P); }
+constexpr int PART = 128;  // partial-projection row pitch (2 x 49 used)
 
 // The GEMM h_{t-1} W_hh^T runs on bf16 MFMA with 3-way split operands (see k_enc_v3): h arrives
 // already split (hsp_in, written by the previous step's epilogue or k_split_rows) and W_hh is
@@ -915,7 +910,7 @@ constexpr int LS_CP = 68;  // k_lstm LDS tile pitch (floats): conflict-free cell
 constexpr int LS_HP = 68;    // pitch of the transposed h' / s tiles [unit][row]: conflict-free MFMA A reads
 constexpr int LS_WSP = 100;  // 98 projection outputs padded to whole float4s
 constexpr int LS_TAIL_FLOATS = 2 * 16 * LS_HP + 16 * LS_WSP;
-template <int H, bool FWT = false>  // FWT: h / s / partials written through whatever AA_WT (the fused attention reads them)
+template <int H>
 __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const float (&gate)[4][2], float2 sa, float2 sb,
                                                float2 cprev, float4 wsv, float* Hs, float* h_out,
                                                bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
@@ -951,9 +946,9 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
     Ss[u0 * HP + rr] = sn[0];
     Ss[(u0 + 1) * HP + rr] = sn[1];
     if (m < B) {
-      st_wt<FWT ? 3 : 2>(reinterpret_cast<float2*>(c_out + (int64_t)m * H + j), make_float2(cn[0], cn[1]));
-      st_wt<FWT ? 0 : 2>(reinterpret_cast<float2*>(h_out + (int64_t)m * H + j), make_float2(hn[0], hn[1]));
-      st_wt<FWT ? 0 : 2>(reinterpret_cast<float2*>(s_out + (int64_t)m * H + j), make_float2(sn[0], sn[1]));
+      st_wt<2>(reinterpret_cast<float2*>(c_out + (int64_t)m * H + j), make_float2(cn[0], cn[1]));
+      st_wt<2>(reinterpret_cast<float2*>(h_out + (int64_t)m * H + j), make_float2(hn[0], hn[1]));
+      st_wt<2>(reinterpret_cast<float2*>(s_out + (int64_t)m * H + j), make_float2(sn[0], sn[1]));
       if (hsp_out) {
         // next step's A fragments: k = j.. in chunk nt, lane (m % 32) + 32 * (u0 / 8), elements u0 % 8..
         typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -966,9 +961,9 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
         }
         bf16x8* o = hsp_out + ((size_t)((m >> 5) * KC + nt) * 3) * 64 + (m & 31) + 32 * (u0 >> 3);
         const int e = u0 & 7;
-        st_wt<FWT ? 3 : 2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e), p0);
-        st_wt<FWT ? 3 : 2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e), p1);
-        st_wt<FWT ? 3 : 2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e), p2);
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o) + e), p0);
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 64) + e), p1);
+        st_wt<2>(reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(o + 128) + e), p2);
       }
     }
   }
@@ -989,12 +984,12 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
       const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
       pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
     }
-    // (all 32 lanes store: columns jj >= P hold exact zeros -- their W values are 0 -- and complete the lines)
-    const int col = (cb < 2 ? 0 : 64) + jj;
+    if (jj < P) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mr = m0 + rb * 32 + acc_row(r, lane);
-      if (mr < B) st_wt<FWT ? 0 : 1>(&part[((int64_t)mr * NTn + nt) * PART + col], pacc[r]);
+      for (int r = 0; r < 16; ++r) {
+        const int mr = m0 + rb * 32 + acc_row(r, lane);
+        if (mr < B) st_wt<1>(&part[((int64_t)mr * NTn + nt) * PART + jg], pacc[r]);
+      }
     }
   }
 }
@@ -1142,237 +1137,6 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
   }
 }
 
-// The arithmetic of one attention row once its operands are in registers, shared by k_atten5 and
-// the attention role of the fused launch k_lstm<.., AT> (so the two produce the same bits).  Thread t
-// (512 per row): projection group grp = t >> 7, output jp = t & 127 (pv: its H/64 tile partials, tiles
-// grp, grp + 4, ...); score item k = t >> 3, lane q = t & 7 (vwr / whr: its 7 terms j = q + 8 i);
-// context dimensions t + 512 i (hv, sv; V through vget(i, kk)).  The 32 projection partials are summed
-// by the four groups, then (g0 + g1) + (g2 + g3); each of the 50 scores by 8 lanes, xor-butterfly.
-// LVL: the st_wt level of the u / norm stores.
-struct AttSmem {
-  float red[4][128];
-  float proj[PART];
-  float zs[PP];
-  float alpha[PP];
-  float norm[16];
-  float beta;
-};
-template <int H, int LVL, class VG>
-__device__ __forceinline__ void atten_row_math(int B, int b, const float (&pv)[H / 64], const float (&vwr)[7],
-                                               const float (&whr)[7], const float (&hv)[H / 512],
-                                               const float (&sv)[H / 512], VG&& vget, AttSmem& sm,
-                                               float* __restrict__ alpha_out, int64_t alpha_ld,
-                                               float* __restrict__ beta_out, int64_t beta_ld, float* __restrict__ u_out,
-                                               uint16_t* __restrict__ ub_out, float* __restrict__ unorm,
-                                               bf16x8* __restrict__ ub3_out) {
-  constexpr int DPT = H / 512, NG = H / 64;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int grp = t >> 7, jp = t & 127, k = t >> 3, q = t & 7;
-  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
-  {
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < NG; ++i) a += pv[i];
-    sm.red[grp][jp] = a;
-  }
-  __syncthreads();
-  AA_TS(1, 1);
-  if (t < 2 * P) sm.proj[t] = (sm.red[0][t] + sm.red[1][t]) + (sm.red[2][t] + sm.red[3][t]);
-  __syncthreads();
-  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
-  {
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
-      const float x = (k < P ? vwr[i] : sm.proj[P + j]) + sm.proj[j];
-      z = __builtin_fmaf(whr[i], tanhf(x), z);
-    }
-    z = z + __shfl_xor(z, 1, 64);
-    z = z + __shfl_xor(z, 2, 64);
-    z = z + __shfl_xor(z, 4, 64);
-    if (q == 0 && k <= P) sm.zs[k] = z;
-  }
-  __syncthreads();
-  AA_TS(1, 2);
-  // 3) softmax (wave 0)
-  if (w == 0) {
-    const float z = lane < P ? sm.zs[lane] : -INFINITY;
-    const float zsn = sm.zs[P];
-    const float m = wave_max(z);
-    const float e = lane < P ? expf(z - m) : 0.f;
-    const float S = wave_sum(e);
-    const float a = e / S;
-    if (lane < P) {
-      sm.alpha[lane] = a;
-      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
-    }
-    const float m2 = fmaxf(m, zsn);
-    const float e2 = lane < P ? expf(z - m2) : 0.f;
-    const float es = expf(zsn - m2);
-    const float S2 = wave_sum(e2) + es;
-    if (lane == 0) {
-      const float beta = es / S2;
-      sm.beta = beta;
-      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
-    }
-  }
-  __syncthreads();
-  AA_TS(1, 3);
-  // 4) context + u
-  const float beta = sm.beta;
-  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
-#pragma unroll
-  for (int i = 0; i < DPT; ++i) {
-    const int d = t + 512 * i;
-    float c = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sm.alpha[kk], vget(i, kk), c);
-    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
-    const float u = chat + hv[i];
-    nsq = __builtin_fmaf(u, u, nsq);
-    st_wt<LVL>(&u_out[(int64_t)b * H + d], u);
-    if (ub_out) {
-      const uint16_t ubv = f2bf(u);
-      ub_out[frag_off(b, d, H)] = ubv;  // (2-byte: plain)
-      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
-      dsq = __builtin_fmaf(du, du, dsq);
-    }
-    if (ub3_out) {
-      __bf16 x0, x1, x2;
-      split3(u, x0, x1, x2);
-      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
-                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
-      o[0] = x0;
-      o[64 * 8] = x1;
-      o[128 * 8] = x2;
-    }
-  }
-  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
-    nsq = wave_sum(nsq);
-    dsq = wave_sum(dsq);
-    if (lane == 0) sm.norm[w] = nsq, sm.norm[8 + w] = dsq;
-    __syncthreads();
-    if (t == 0) {
-      const float* n = sm.norm;
-      st_wt<LVL>(&unorm[b], sqrtf(((n[0] + n[1]) + (n[2] + n[3])) + ((n[4] + n[5]) + (n[6] + n[7]))) * 1.0001f);
-      st_wt<LVL>(&unorm[B + b],
-                 sqrtf(((n[8] + n[9]) + (n[10] + n[11])) + ((n[12] + n[13]) + (n[14] + n[15]))) * 1.0001f);
-    }
-  }
-  AA_TS(1, 4);
-}
-
-// Two rows (A, B) through atten_row_math's phases together: each phase of both rows, then one
-// barrier (four barriers for the pair instead of eight; the softmax of row A on wave 0, of row B on
-// wave 1).  Every row's arithmetic is atten_row_math's, in the same order: the same bits.  H = 512.
-template <int LVL, class VGA, class VGB>
-__device__ __forceinline__ void atten_rows2_math(int B, int rA, int rB, bool two, const float (&pa)[8],
-                                                 const float (&pb)[8], const float (&vwa)[7], const float (&vwb)[7],
-                                                 const float (&whr)[7], float ha, float sa, float hb, float sb,
-                                                 VGA&& vga, VGB&& vgb, AttSmem (&sm)[2], float* __restrict__ alpha_out,
-                                                 int64_t alpha_ld, float* __restrict__ beta_out, int64_t beta_ld,
-                                                 float* __restrict__ u_out, uint16_t* __restrict__ ub_out,
-                                                 float* __restrict__ unorm) {
-  constexpr int H = 512;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int grp = t >> 7, jp = t & 127, k = t >> 3, q = t & 7;
-  {
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a += pa[i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b += pb[i];
-    sm[0].red[grp][jp] = a;
-    sm[1].red[grp][jp] = b;
-  }
-  __syncthreads();
-  if (t < 2 * P) sm[0].proj[t] = (sm[0].red[0][t] + sm[0].red[1][t]) + (sm[0].red[2][t] + sm[0].red[3][t]);
-  if (t >= 256 && t < 256 + 2 * P) {
-    const int j = t - 256;
-    sm[1].proj[j] = (sm[1].red[0][j] + sm[1].red[1][j]) + (sm[1].red[2][j] + sm[1].red[3][j]);
-  }
-  __syncthreads();
-  {
-    float za = 0.f, zb = 0.f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
-      const float xa = (k < P ? vwa[i] : sm[0].proj[P + j]) + sm[0].proj[j];
-      const float xb = (k < P ? vwb[i] : sm[1].proj[P + j]) + sm[1].proj[j];
-      za = __builtin_fmaf(whr[i], tanhf(xa), za);
-      zb = __builtin_fmaf(whr[i], tanhf(xb), zb);
-    }
-    za = za + __shfl_xor(za, 1, 64);
-    zb = zb + __shfl_xor(zb, 1, 64);
-    za = za + __shfl_xor(za, 2, 64);
-    zb = zb + __shfl_xor(zb, 2, 64);
-    za = za + __shfl_xor(za, 4, 64);
-    zb = zb + __shfl_xor(zb, 4, 64);
-    if (q == 0 && k <= P) sm[0].zs[k] = za, sm[1].zs[k] = zb;
-  }
-  __syncthreads();
-  if (w < 2 && (w == 0 || two)) {  // softmax: wave 0 row A, wave 1 row B
-    AttSmem& x = sm[w];
-    const int b = w ? rB : rA;
-    const float z = lane < P ? x.zs[lane] : -INFINITY;
-    const float zsn = x.zs[P];
-    const float m = wave_max(z);
-    const float e = lane < P ? expf(z - m) : 0.f;
-    const float S = wave_sum(e);
-    const float a = e / S;
-    if (lane < P) {
-      x.alpha[lane] = a;
-      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
-    }
-    const float m2 = fmaxf(m, zsn);
-    const float e2 = lane < P ? expf(z - m2) : 0.f;
-    const float es = expf(zsn - m2);
-    const float S2 = wave_sum(e2) + es;
-    if (lane == 0) {
-      const float beta = es / S2;
-      x.beta = beta;
-      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
-    }
-  }
-  __syncthreads();
-  float nsq[2] = {0.f, 0.f}, dsq[2] = {0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    if (r == 1 && !two) break;
-    const int b = r ? rB : rA;
-    const float beta = sm[r].beta;
-    float c = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sm[r].alpha[kk], r ? vgb(kk) : vga(kk), c);
-    const float chat = __builtin_fmaf(beta, r ? sb : sa, (1.f - beta) * c);
-    const float u = chat + (r ? hb : ha);
-    nsq[r] = __builtin_fmaf(u, u, nsq[r]);
-    st_wt<LVL>(&u_out[(int64_t)b * H + t], u);
-    if (ub_out) {
-      const uint16_t ubv = f2bf(u);
-      ub_out[frag_off(b, t, H)] = ubv;
-      const float du = u - __uint_as_float((uint32_t)ubv << 16);
-      dsq[r] = __builtin_fmaf(du, du, dsq[r]);
-    }
-  }
-  if (unorm) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const float n2 = wave_sum(nsq[r]), d2 = wave_sum(dsq[r]);
-      if (lane == 0) sm[r].norm[w] = n2, sm[r].norm[8 + w] = d2;
-    }
-    __syncthreads();
-    if (t == 0 || (t == 64 && two)) {
-      const float* n = sm[t >> 6].norm;
-      const int b = t ? rB : rA;
-      st_wt<LVL>(&unorm[b], sqrtf(((n[0] + n[1]) + (n[2] + n[3])) + ((n[4] + n[5]) + (n[6] + n[7]))) * 1.0001f);
-      st_wt<LVL>(&unorm[B + b],
-                 sqrtf(((n[8] + n[9]) + (n[10] + n[11])) + ((n[12] + n[13]) + (n[14] + n[15]))) * 1.0001f);
-    }
-  }
-}
-
 // G (beam search): row m continues the hypothesis of row par[m] of the previous step, so its h
 // fragments and c are gathered from that row (the beams of an image are adjacent rows, so the
 // gathered 16-B fragment loads stay within the same or the neighbouring 32-row block).
@@ -1412,215 +1176,7 @@ constexpr uint64_t RS_WAIT_TICKS = 5000;  // 50 us of the 100 MHz constant clock
 #ifndef LS_RS_JG
 #define LS_RS_JG (LS_RS_JK + 3)
 #endif
-// ---------------------------------------------------------------------------------------------
-// The attention of step t inside step t's LSTM launch (k_lstm<512, .., AT>).
-// The launch's first NR workgroups (which also rescore step t-1 when RS) each run the attention of
-// rows 2 bid, 2 bid + 1: they issue the loads that do not depend on this step's LSTM -- both rows' V
-// (row A in VGPRs, row B's first AT_NL positions by LDS-DMA, the rest in VGPRs), VWv, w_h -- so the
-// 51 MB V stream runs under the GEMM workgroups' h W_hh^T ring, then wait (bounded) on their row
-// block's arrival counter.  Each GEMM workgroup writes its h / s / projection partials through (sc1),
-// drains them (vmcnt(0)) and bumps its row block's counter by one agent-scope atomic; the partials,
-// h and s are then read with agent-coherent loads.  The row arithmetic is atten_row_math, as in
-// k_atten5, so the fused and split launch structures give the same bits (AA_DECODE_SPLIT_ATTEN).
-// No workgroup waits unboundedly: an attention workgroup that sees no ready block within at.wait
-// exits; the LAST arriver of each row block then waits at most at.grace for the block's rows to be
-// claimed (an attention workgroup claims its rows when it sees the block ready) and computes every
-// unclaimed row itself -- the same function on the same inputs, so a row computed twice is written
-// twice with the same values.  Every row is therefore computed whatever the dispatch order or
-// co-residency (no cooperative launch needed).
-struct AtArgs {
-  const float* V;    // [B][P][H] (k_enc_v4)
-  const float* vwv;  // [B][P][PP]
-  const float* wh;   // [PP]
-  float* alpha;      // this step's alpha (row stride alpha_ld) or nullptr
-  int64_t alpha_ld;
-  float* beta;
-  int64_t beta_ld;
-  float* u;          // this step's u [B][H]
-  uint16_t* ub;      // bf16 u, fragment order
-  float* unorm;      // [2][B]
-  uint64_t* arr;     // [MT] arrival counters of this step (zeroed before the decode)
-  uint64_t* done;    // [B] rows claimed (zeroed before the decode)
-  uint64_t wait;     // attention workgroups' bound on their wait (ticks of the 100 MHz clock)
-  uint64_t grace;    // the last arriver's bound on its wait for the claims
-};
-#ifndef AA_AT_NL
-#define AA_AT_NL 36
-#endif
-#ifndef AA_AT_LATE
-#define AA_AT_LATE 0
-#endif
-// positions of row B's V staged in LDS (36 x 2 KB beside the two rows' scratch: 78.1 KB per
-// workgroup, two per CU); the other 13 in VGPRs
-constexpr int AT_NL = AA_AT_NL;
-constexpr uint64_t AT_WAIT_TICKS = 5000, AT_GRACE_TICKS = 3000;  // 50 us, 30 us
-
-// agent-coherent 4-byte load (global_load_dword sc1): data written through by other XCDs' workgroups
-// of the same launch
-__device__ __forceinline__ float ld_ac(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// This step's LSTM outputs of row r for atten_row_math (thread t: tiles grp + 4 i of output jp,
-// context dimension t), read coherently.
-template <int H>
-__device__ __forceinline__ void atten_lstm_operands(int r, const float* __restrict__ h_new,
-                                                    const float* __restrict__ s_new, const float* __restrict__ part,
-                                                    float (&pv)[H / 64], float (&hv)[1], float (&sv)[1]) {
-  constexpr int NT16 = H / 16;
-  const int t = threadIdx.x, grp = t >> 7, jp = t & 127, jpc = part_col(jp < 2 * P ? jp : 2 * P - 1);
-  const float* pp = part + ((int64_t)r * NT16 + grp) * PART + jpc;
-#pragma unroll
-  for (int i = 0; i < H / 64; ++i) pv[i] = ld_ac(pp + (int64_t)4 * i * PART);
-  hv[0] = ld_ac(h_new + (int64_t)r * H + t);
-  sv[0] = ld_ac(s_new + (int64_t)r * H + t);
-}
-// VWv row terms and w_h of score item k = t >> 3, lane q = t & 7 (as k_atten5 loads them)
-__device__ __forceinline__ void atten_score_operands(const float* __restrict__ vwv, const float* __restrict__ wh, int img,
-                                                     float (&vwr)[7], float (&whr)[7]) {
-  const int t = threadIdx.x, k = t >> 3, q = t & 7, kc = k < P ? k : P - 1;
-  const float* vw = vwv + ((int64_t)img * P + kc) * PP;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int j = q + 8 * i < P ? q + 8 * i : P - 1;
-    vwr[i] = vw[j];
-    whr[i] = q + 8 * i < P ? wh[j] : 0.f;
-  }
-}
-
-template <int H>
-__device__ __forceinline__ void atten_role(int B, int bid, const float* __restrict__ h_new,
-                                           const float* __restrict__ s_new, const float* __restrict__ part,
-                                           const AtArgs& at, float* lds) {
-  static_assert(H == 512, "one context dimension per thread");
-  constexpr int NT16 = H / 16, NL = AT_NL, NV = P - NL;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int rA = 2 * bid, rB = rA + 1;
-  if (rA >= B) return;  // (workgroup-uniform) a padding workgroup
-  const bool two = rB < B;
-  const int mt = rA >> 6;  // rB is in the same 64-row block
-  AttSmem (&sm2)[2] = *reinterpret_cast<AttSmem(*)[2]>(lds + NL * H);
-  uint32_t* ready = reinterpret_cast<uint32_t*>(lds + NL * H + 2 * sizeof(AttSmem) / 4);
-  // 1) what does not depend on this step's LSTM, oldest first: row A's V, row B's V, VWv, w_h
-  const float* vbA = at.V + (int64_t)rA * P * H;
-  const float* vbB = at.V + (int64_t)(two ? rB : rA) * P * H;
-  float va[P], vr[NV];
-  auto load_v = [&] {
-#pragma unroll
-    for (int kk = 0; kk < P; ++kk) va[kk] = vbA[(int64_t)kk * H + t];
-    for (int i = wave; i < 2 * NL; i += 8) {  // position i / 2, half i % 2: one 1-KB wave instruction
-      const int pp = i >> 1, hh = i & 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbB + (int64_t)pp * H + hh * 256 + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(lds + pp * H + hh * 256), 16, 0, 0);
-    }
-#pragma unroll
-    for (int kk = 0; kk < NV; ++kk) vr[kk] = vbB[(int64_t)(NL + kk) * H + t];
-  };
-#ifndef AA_AT_PF
-#define AA_AT_PF 1
-#endif
-  if constexpr (AA_AT_PF) load_v();  // (AA_AT_PF 0: V only once the block is ready -- a probe)
-  float vwa[7], whr[7];
-  atten_score_operands(at.vwv, at.wh, rA, vwa, whr);
-  AA_TS(4, 2);
-  // 2) the row block's NT16 tiles (bounded wait), then claim the rows
-  if (t == 0) {
-    uint64_t n = __hip_atomic_load(at.arr + mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t t0 = wall_clock64();
-    while (n < (uint64_t)NT16 && wall_clock64() - t0 <= at.wait) {
-      __builtin_amdgcn_s_sleep(2);
-      n = __hip_atomic_load(at.arr + mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const bool ok = n >= (uint64_t)NT16;
-    if (ok) {
-      __hip_atomic_store(at.done + rA, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (two) __hip_atomic_store(at.done + rB, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *ready = ok ? 1u : 0u;
-  }
-  __syncthreads();  // (drains every wave's loads and LDS-DMAs: safe to exit, and row B's V is in LDS)
-  AA_TS(4, 3);
-  AA_TSV(4, *ready ? 1 : 2);
-  if (!*ready) return;  // the row block's last arriver computes these rows
-  if constexpr (!AA_AT_PF) {
-    load_v();
-    __syncthreads();
-  }
-  // 3) this step's LSTM outputs (agent-coherent), then the two rows
-  // (AA_AT_LATE: row B's operands are loaded after row A's arithmetic -- fewer live VGPRs)
-  float pa[H / 64], ha[1], sa[1];
-  atten_lstm_operands<H>(rA, h_new, s_new, part, pa, ha, sa);
-  float pb[H / 64], hb[1], sb[1], vwb[7];
-  if constexpr (!AA_AT_LATE) {
-    atten_lstm_operands<H>(two ? rB : rA, h_new, s_new, part, pb, hb, sb);
-    atten_score_operands(at.vwv, at.wh, two ? rB : rA, vwb, whr);
-  }
-#ifndef AA_AT_PAIR
-#define AA_AT_PAIR 1
-#endif
-  if constexpr (AA_AT_PAIR && !AA_AT_LATE) {  // both rows' phases together
-    atten_rows2_math<3>(B, rA, rB, two, pa, pb, vwa, vwb, whr, ha[0], sa[0], hb[0], sb[0],
-                        [&](int kk) { return va[kk]; },
-                        [&](int kk) { return kk < NL ? lds[kk * H + t] : vr[kk - NL]; }, sm2, at.alpha, at.alpha_ld,
-                        at.beta, at.beta_ld, at.u, at.ub, at.unorm);
-    AA_TS(4, 4);
-    return;
-  }
-  AttSmem& sm = sm2[0];
-  atten_row_math<H, 3>(B, rA, pa, vwa, whr, ha, sa, [&](int, int kk) { return va[kk]; }, sm,
-                       at.alpha, at.alpha_ld, at.beta, at.beta_ld, at.u, at.ub, at.unorm, nullptr);
-  AA_TS(4, 4);
-  if (!two) return;
-  if constexpr (AA_AT_LATE) {
-    atten_lstm_operands<H>(rB, h_new, s_new, part, pb, hb, sb);
-    atten_score_operands(at.vwv, at.wh, rB, vwb, whr);
-  }
-  atten_row_math<H, 3>(B, rB, pb, vwb, whr, hb, sb,
-                       [&](int, int kk) { return kk < NL ? lds[kk * H + t] : vr[kk - NL]; }, sm, at.alpha,
-                       at.alpha_ld, at.beta, at.beta_ld, at.u, at.ub, at.unorm, nullptr);
-}
-
-// The last arriver of row block m0 / 64: wait at most at.grace for the block's rows to be claimed, then
-// compute every unclaimed row (one at a time, V from memory).
-template <int H>
-__device__ __forceinline__ void atten_rows_fallback(int B, int m0, const float* __restrict__ h_new,
-                                                 const float* __restrict__ s_new, const float* __restrict__ part,
-                                                 const AtArgs& at, float* lds) {
-  const int t = threadIdx.x;
-  uint64_t* mask = reinterpret_cast<uint64_t*>(lds);
-  AttSmem& sm = *reinterpret_cast<AttSmem*>(lds + 4);
-  if (t < 64) {
-    const int r = m0 + t;
-    uint64_t d = r < B ? __hip_atomic_load(at.done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1ull;
-    const uint64_t t0 = wall_clock64();
-    while (!__all(d != 0) && wall_clock64() - t0 <= at.grace) {  // wave-uniform
-      __builtin_amdgcn_s_sleep(2);
-      if (d == 0) d = __hip_atomic_load(at.done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint64_t mb = __ballot(d == 0);
-    if (t == 0) *mask = mb;
-  }
-  __syncthreads();
-  uint64_t mb = *mask;
-  while (mb) {  // (workgroup-uniform)
-    const int r = m0 + __builtin_ctzll(mb);
-    mb &= mb - 1;
-    float vv[P];
-    const float* vb = at.V + (int64_t)r * P * H;
-#pragma unroll
-    for (int kk = 0; kk < P; ++kk) vv[kk] = vb[(int64_t)kk * H + t];
-    float vwr[7], whr[7];
-    atten_score_operands(at.vwv, at.wh, r, vwr, whr);
-    float pv[H / 64], hv[1], sv[1];
-    atten_lstm_operands<H>(r, h_new, s_new, part, pv, hv, sv);
-    atten_row_math<H, 3>(B, r, pv, vwr, whr, hv, sv, [&](int, int kk) { return vv[kk]; }, sm, at.alpha,
-                         at.alpha_ld, at.beta, at.beta_ld, at.u, at.ub, at.unorm, nullptr);
-    __syncthreads();  // sm is reused by the next row
-  }
-}
-
-template <int H, bool G = false, bool RS = false, bool AT = false>
+template <int H, bool G = false, bool RS = false>
 __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const int64_t* __restrict__ tok, int tok_ld,
                                               const float* __restrict__ table,
                                               const float* __restrict__ xg, const bf16x8* __restrict__ hsp_in,
@@ -1628,41 +1184,28 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
                                               const bf16x8* __restrict__ whh3,
                                               const float* __restrict__ wgs, float* __restrict__ h_out,
                                               bf16x8* __restrict__ hsp_out, float* __restrict__ c_out,
-                                              float* __restrict__ s_out, float* __restrict__ part, RsArgs ra,
-                                              AtArgs at) {
+                                              float* __restrict__ s_out, float* __restrict__ part, RsArgs ra) {
   constexpr int BM = 64, CP = LS_CP, TS = 64 * LS_CP;
   AA_TS(0, 0);
   // the LDS-DMA ring of lstm_gemm_lds (72 KB; the summed tile and the cell tail alias it)
   constexpr int RING_FLOATS = (LS_NB < H / 32 ? LS_NB : H / 32) * LS_STAGE * 4;
   // + the tile's 64 tokens (+ RS: the missing-row mask and slow-path flag, the 64 keys' low words
   // DMA'd mid-ring)
-  constexpr int LDS_FLOATS0 = RING_FLOATS + 64 + 4 + (RS ? 64 : 0);
-  // AT: the attention role's row B V positions, row scratch and ready flag (<= 80 KB: two per CU)
-  constexpr int AT_FLOATS = AT ? AT_NL * H + (int)(2 * sizeof(AttSmem) / 4) + 4 : 0;
-  constexpr int LDS_FLOATS = LDS_FLOATS0 > AT_FLOATS ? LDS_FLOATS0 : AT_FLOATS;
-  static_assert(LDS_FLOATS * 4 <= 80 * 1024, "two workgroups per CU");
+  constexpr int LDS_FLOATS = RING_FLOATS + 64 + 4 + (RS ? 64 : 0);
   static_assert(TS + LS_TAIL_FLOATS <= LDS_FLOATS, "tile + tail must fit in the ring");
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   constexpr int NTn = H / 16, KC = H / 16;
   const int MT = (B + BM - 1) / BM;
   int bid = blockIdx.x;
-  if constexpr (RS || AT) {
-    static_assert(!G, "the fused rescoring / attention is the greedy path's");
-    static_assert(!RS || TS + 2 * RsScratch<H>::FLOATS <= RING_FLOATS, "two rescoring scratch areas beside the tile");
-    static_assert(!AT || H == 512, "the attention role: one context dimension per thread");
-    if (bid < ra.NR) {  // rescoring / attention role (uniform per workgroup): rows 2 bid, 2 bid + 1
-      if constexpr (RS) {  // rows 2 bid + (t >> 8) of step t - 1
-        AA_TS(4, 0);
-        const int row = 2 * bid + (int)(threadIdx.x >> 8);
-        rescore_row<H, true>(row < B ? row : B - 1, row < B, threadIdx.x & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
-                             ra.bias, ra.keys, ra.ids, ra.T, ra.t_step, lds + (threadIdx.x >> 8) * RsScratch<H>::FLOATS);
-        AA_TS(4, 1);
-      }
-      if constexpr (AT) {
-        if constexpr (RS) __syncthreads();  // the rescoring scratch is free
-        atten_role<H>(B, bid, h_out, s_out, part, at, lds);
-        AA_TS(4, 5);
-      }
+  if constexpr (RS) {
+    static_assert(!G, "the fused rescoring is the greedy path's");
+    static_assert(TS + 2 * RsScratch<H>::FLOATS <= RING_FLOATS, "two rescoring scratch areas beside the tile");
+    if (bid < ra.NR) {  // rescoring role (uniform per workgroup): rows 2 bid + (t >> 8)
+      AA_TS(4, 0);
+      const int row = 2 * bid + (int)(threadIdx.x >> 8);
+      rescore_row<H, true>(row < B ? row : B - 1, row < B, threadIdx.x & 255, V, ra.Vp, ra.u, ra.summ, ra.W,
+                           ra.bias, ra.keys, ra.ids, ra.T, ra.t_step, lds + (threadIdx.x >> 8) * RsScratch<H>::FLOATS);
+      AA_TS(4, 1);
       return;
     }
     bid -= ra.NR;
@@ -1824,21 +1367,8 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
       for (int q = 0; q < 2; ++q) gate[g][q] = cr[(16 * g + u0 + q) * CP] + ((&ta[g].x)[q] + (&xa[g].x)[q]);
   }
   AA_TS(0, 2);
-  lstm_cell_tail<H, AT>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + TS, h_out, hsp_out, c_out, s_out, part);
+  lstm_cell_tail<H>(B, m0, nt, gate, sa, sb, cprev, wsv, lds + TS, h_out, hsp_out, c_out, s_out, part);
   AA_TS(0, 4);
-  if constexpr (AT) {  // publish the tile to the row block's attention: stores acknowledged, then one arrival
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint32_t* last = reinterpret_cast<uint32_t*>(lds + RING_FLOATS);  // (the token slots: free now)
-    if (t == 0) {
-      const uint64_t old = __hip_atomic_fetch_add(at.arr + mt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *last = old == (uint64_t)(NTn - 1) ? 1u : 0u;
-    }
-    __syncthreads();
-    AA_TSV(0, *last ? 1 : 0);
-    if (*last) atten_rows_fallback<H>(B, m0, h_out, s_out, part, at, lds);
-    AA_TS(0, 6);
-  }
 }
 
 __global__ void k_fill_tok(int64_t* __restrict__ tok, int B, int64_t v) {
@@ -1913,7 +1443,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   //  for partials + VWv, while the 98 V values of this thread stay in flight.)  No branches
   //  around loads: out-of-range lanes read clamped addresses and their values are never used.
   constexpr int NT16 = H / 16;  // == NTL
-  const int tp = part_col(t < 2 * P ? t : 2 * P - 1);
+  const int tp = t < 2 * P ? t : 2 * P - 1;
   float pv[NT16];
   {
     const float* pp = part + (int64_t)b * NT16 * PART + tp;
@@ -2030,6 +1560,127 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   }
 }
 
+// The arithmetic of one attention row once its operands are in registers, shared by k_atten5 and
+// the attention role of the fused launch k_lstm<.., AT> (so the two produce the same bits).  Thread t
+// (512 per row): projection group grp = t >> 7, output jp = t & 127 (pv: its H/64 tile partials, tiles
+// grp, grp + 4, ...); score item k = t >> 3, lane q = t & 7 (vwr / whr: its 7 terms j = q + 8 i);
+// context dimensions t + 512 i (hv, sv; V through vget(i, kk)).  The 32 projection partials are summed
+// by the four groups, then (g0 + g1) + (g2 + g3); each of the 50 scores by 8 lanes, xor-butterfly.
+// LVL: the st_wt level of the u / norm stores.
+struct AttSmem {
+  float red[4][128];
+  float proj[PART];
+  float zs[PP];
+  float alpha[PP];
+  float norm[16];
+  float beta;
+};
+template <int H, int LVL, class VG>
+__device__ __forceinline__ void atten_row_math(int B, int b, const float (&pv)[H / 64], const float (&vwr)[7],
+                                               const float (&whr)[7], const float (&hv)[H / 512],
+                                               const float (&sv)[H / 512], VG&& vget, AttSmem& sm,
+                                               float* __restrict__ alpha_out, int64_t alpha_ld,
+                                               float* __restrict__ beta_out, int64_t beta_ld, float* __restrict__ u_out,
+                                               uint16_t* __restrict__ ub_out, float* __restrict__ unorm,
+                                               bf16x8* __restrict__ ub3_out) {
+  constexpr int DPT = H / 512, NG = H / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int grp = t >> 7, jp = t & 127, k = t >> 3, q = t & 7;
+  // 1) projections: tile partials in four fixed groups (tiles grp, grp + 4, ...), groups combined
+  {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) a += pv[i];
+    sm.red[grp][jp] = a;
+  }
+  __syncthreads();
+  AA_TS(1, 1);
+  if (t < 2 * P) sm.proj[t] = (sm.red[0][t] + sm.red[1][t]) + (sm.red[2][t] + sm.red[3][t]);
+  __syncthreads();
+  // 2) scores: item k (0..49) by 8 lanes, j = q + 8i
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = q + 8 * i < P ? q + 8 * i : P - 1;
+      const float x = (k < P ? vwr[i] : sm.proj[P + j]) + sm.proj[j];
+      z = __builtin_fmaf(whr[i], tanhf(x), z);
+    }
+    z = z + __shfl_xor(z, 1, 64);
+    z = z + __shfl_xor(z, 2, 64);
+    z = z + __shfl_xor(z, 4, 64);
+    if (q == 0 && k <= P) sm.zs[k] = z;
+  }
+  __syncthreads();
+  AA_TS(1, 2);
+  // 3) softmax (wave 0)
+  if (w == 0) {
+    const float z = lane < P ? sm.zs[lane] : -INFINITY;
+    const float zsn = sm.zs[P];
+    const float m = wave_max(z);
+    const float e = lane < P ? expf(z - m) : 0.f;
+    const float S = wave_sum(e);
+    const float a = e / S;
+    if (lane < P) {
+      sm.alpha[lane] = a;
+      if (alpha_out) alpha_out[(int64_t)b * alpha_ld + lane] = a;
+    }
+    const float m2 = fmaxf(m, zsn);
+    const float e2 = lane < P ? expf(z - m2) : 0.f;
+    const float es = expf(zsn - m2);
+    const float S2 = wave_sum(e2) + es;
+    if (lane == 0) {
+      const float beta = es / S2;
+      sm.beta = beta;
+      if (beta_out) beta_out[(int64_t)b * beta_ld] = beta;
+    }
+  }
+  __syncthreads();
+  AA_TS(1, 3);
+  // 4) context + u
+  const float beta = sm.beta;
+  float nsq = 0.f, dsq = 0.f;  // ||u||^2 and ||u - bf16(u)||^2 (the screen's bound)
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int d = t + 512 * i;
+    float c = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) c = __builtin_fmaf(sm.alpha[kk], vget(i, kk), c);
+    const float chat = __builtin_fmaf(beta, sv[i], (1.f - beta) * c);
+    const float u = chat + hv[i];
+    nsq = __builtin_fmaf(u, u, nsq);
+    st_wt<LVL>(&u_out[(int64_t)b * H + d], u);
+    if (ub_out) {
+      const uint16_t ubv = f2bf(u);
+      ub_out[frag_off(b, d, H)] = ubv;  // (2-byte: plain)
+      const float du = u - __uint_as_float((uint32_t)ubv << 16);  // exact (Sterbenz)
+      dsq = __builtin_fmaf(du, du, dsq);
+    }
+    if (ub3_out) {
+      __bf16 x0, x1, x2;
+      split3(u, x0, x1, x2);
+      __bf16* o = reinterpret_cast<__bf16*>(ub3_out + ((size_t)((b >> 5) * (H / 16) + (d >> 4)) * 3) * 64 +
+                                            (b & 31) + 32 * ((d >> 3) & 1)) + (d & 7);
+      o[0] = x0;
+      o[64 * 8] = x1;
+      o[128 * 8] = x2;
+    }
+  }
+  if (unorm) {  // [2][B]: ||u||, ||u - bf16(u)||, each inflated over its fp32 rounding (gamma_H < 1e-4)
+    nsq = wave_sum(nsq);
+    dsq = wave_sum(dsq);
+    if (lane == 0) sm.norm[w] = nsq, sm.norm[8 + w] = dsq;
+    __syncthreads();
+    if (t == 0) {
+      const float* n = sm.norm;
+      st_wt<LVL>(&unorm[b], sqrtf(((n[0] + n[1]) + (n[2] + n[3])) + ((n[4] + n[5]) + (n[6] + n[7]))) * 1.0001f);
+      st_wt<LVL>(&unorm[B + b],
+                 sqrtf(((n[8] + n[9]) + (n[10] + n[11])) + ((n[12] + n[13]) + (n[14] + n[15]))) * 1.0001f);
+    }
+  }
+  AA_TS(1, 4);
+}
+
 // k_atten with two threads per output dimension's worth of parallelism: 512 threads per row, each
 // owning H/512 dimensions of the context (half the V registers of k_atten<2>, twice the waves in
 // flight per CU), the 32 projection partials summed by four groups of 128 threads (8 each, then
@@ -2050,7 +1701,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
   // loads, oldest first in the order they are consumed; clamped addresses, no branches
-  const int grp = t >> 7, jp = t & 127, jpc = part_col(jp < 2 * P ? jp : 2 * P - 1);
+  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
   float pv[NG];
   {
     const float* pp = part + ((int64_t)b * NT16 + grp) * PART + jpc;
@@ -2117,7 +1768,7 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
   __shared__ float sh_norm[KB][16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int img = blockIdx.x, r0 = img * KB;
-  const int grp = t >> 7, jp = t & 127, jpc = part_col(jp < 2 * P ? jp : 2 * P - 1);
+  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
   float pv[KB][NG];
 #pragma unroll
   for (int r = 0; r < KB; ++r) {
@@ -3346,17 +2997,13 @@ static StepWS carve_step(char* base, const Layout& L, int B, size_t* bytes) {
 }
 
 struct DecodeWS {
-  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u[2], *unorm, *part;
+  float *a_g, *V, *vwv, *vg, *xg, *h[2], *c[2], *s, *u, *unorm, *part;
   uint16_t* ub;
   bf16x8* hsp[2];
   float4* summ;
-  uint64_t* keys;  // [T][B] argmax keys, then the fused attention's [T][B] row claims and [T][MT] arrivals
-  uint64_t *done, *arr;
+  uint64_t* keys;
   int64_t* tok0;
 };
-// u is double-buffered (step t writes u[t & 1]): with the attention inside the LSTM launch, step t's
-// attention writes u while the same launch rescores step t-1 from the other buffer.
-static int sync_words(int B, int T) { return 2 * T * B + T * ((B + 63) / 64); }
 static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* bytes) {
   Carver c{base};
   DecodeWS w;
@@ -3370,15 +3017,13 @@ static DecodeWS carve_decode(char* base, const Layout& L, int B, int T, size_t* 
     w.c[i] = c.take<float>((size_t)B * L.H);
   }
   w.s = c.take<float>((size_t)B * L.H);
-  for (int i = 0; i < 2; ++i) w.u[i] = c.take<float>((size_t)B * L.H);
+  w.u = c.take<float>((size_t)B * L.H);
   w.unorm = c.take<float>((size_t)2 * B);  // ||u|| then ||u - bf16(u)|| per row
   w.part = c.take<float>((size_t)B * (L.H / 16) * PART);
   w.ub = c.take<uint16_t>((size_t)((B + 127) / 128) * 128 * L.H);  // fragment order, 128-row tiles
   for (int i = 0; i < 2; ++i) w.hsp[i] = c.take<bf16x8>(hsp_frags(L, B));
   w.summ = c.take<float4>((size_t)B * (L.Vp / VS_TILE));
-  w.keys = c.take<uint64_t>((size_t)sync_words(B, T));
-  w.done = w.keys + (size_t)T * B;
-  w.arr = w.done + (size_t)T * B;
+  w.keys = c.take<uint64_t>((size_t)T * B);
   w.tok0 = c.take<int64_t>((size_t)B);
   *bytes = c.off;
   return w;
@@ -3403,41 +3048,25 @@ size_t aa_decode_workspace_bytes(const aa_dims* d, int32_t B, int32_t T) {
 // par != nullptr: beam search (rows continue rows par[] of the previous step)
 // ra != nullptr: greedy step t >= 1 with step t-1's rescoring in the same launch (k_lstm<.., RS>); the
 // tokens come from the published keys, `tok` is not read
-// at != nullptr (H = 512 only): the step's attention in the same launch (k_lstm<512, .., AT>: ra->NR
-// attention workgroups first, which also rescore step t-1 when `ra` carries a previous step,
-// ra->t_step >= 0)
 static void lstm_launch(const Layout& L, const MP& p, int B, const int64_t* tok, int tok_ld, const float* xg,
                         const bf16x8* hsp_in, const float* c_in, float* h_out, bf16x8* hsp_out, float* c_out,
                         float* s_buf, float* part, hipStream_t s, const int* par = nullptr,
-                        const RsArgs* ra = nullptr, aa_event_t* ev = nullptr, int ei = 0, const AtArgs* at = nullptr) {
+                        const RsArgs* ra = nullptr, aa_event_t* ev = nullptr, int ei = 0) {
   const int H = L.H, MT = (B + 63) / 64;
   const RsArgs none{};
-  const AtArgs anone{};
   const int64_t* tnull = nullptr;
-  if (at && H == 512) {
-    const dim3 grid(ra->NR + MT * (512 / 16));
-    if (ra->t_step >= 0)
-      AA_TLAUNCH(ev, ei, (k_lstm<512, false, true, true>), grid, dim3(512), 0, s, B, L.V, tnull, 0, p.table, xg,
-                 hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, *ra, *at);
-    else
-      AA_TLAUNCH(ev, ei, (k_lstm<512, false, false, true>), grid, dim3(512), 0, s, B, L.V, tok, tok_ld, p.table, xg,
-                 hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, *ra, *at);
-    return;
-  }
 #define AA_LSTM(H_)                                                                                          \
   do {                                                                                                       \
     if (par)                                                                                                 \
       AA_TLAUNCH(ev, ei, (k_lstm<H_, true>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,     \
-                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none,     \
-                 anone);                                                                                     \
+                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none);    \
     else if (ra)                                                                                             \
       AA_TLAUNCH(ev, ei, (k_lstm<H_, false, true>), dim3(ra->NR + MT * (H_ / 16)), dim3(512), 0, s, B, L.V,   \
                  tnull, 0, p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part,  \
-                 *ra, anone);                                                                                \
+                 *ra);                                                                                       \
     else                                                                                                     \
       AA_TLAUNCH(ev, ei, (k_lstm<H_, false>), dim3(MT * (H_ / 16)), dim3(512), 0, s, B, L.V, tok, tok_ld,    \
-                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none,     \
-                 anone);                                                                                     \
+                 p.table, xg, hsp_in, c_in, par, p.whh3, p.wgs, h_out, hsp_out, c_out, s_buf, part, none);    \
   } while (0)
   switch (H) {
     case 256: AA_LSTM(256); break;
@@ -3547,10 +3176,6 @@ static bool screen_wide(const Layout& L) { return L.Vp % SC2_BN == 0 && L.H <= 5
 // The T-step loop over the B rows: k_lstm (GEMM + cell + attention projections), k_atten, then the
 // vocab stage -- k_vscreen2 (bf16 screen, granule summaries) + k_vrescore (exact fp32 rescoring of
 // the candidates), or with AA_DECODE_EXACT_VOCAB the exact fp32 GEMM k_vocab + k_key_ids.
-// the launch structure of a greedy decode (aa_decode_launch_structure)
-static bool fused_attention(const Layout& L, int32_t flags) {
-  return L.H == 512 && !(flags & (AA_DECODE_EXACT_VOCAB | AA_DECODE_SPLIT_RESCORE | AA_DECODE_SPLIT_ATTEN));
-}
 static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, int T, int32_t flags, int64_t* ids,
                        float* alpha, float* beta, const aa_trace* trace, hipStream_t s) {
   const bool exact = (flags & AA_DECODE_EXACT_VOCAB) != 0;
@@ -3559,8 +3184,6 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   // the rescoring of step t-1 rides in step t's LSTM launch (k_lstm<.., RS>); the last step's has
   // its own launch
   const bool fused = !exact && (flags & AA_DECODE_SPLIT_RESCORE) == 0;
-  // and (H = 512) so does step t's attention (k_lstm<512, .., AT>)
-  const bool fat = fused_attention(L, flags);
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1, nxt = cur ^ 1;
     // token of step t-1: ids[:, t-1] (written by the previous step); t = 0: nullptr = <start> for every row
@@ -3569,23 +3192,17 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
     uint64_t* kt = w.keys + (size_t)t * B;
     float* alt = alpha ? alpha + (size_t)t * P : nullptr;
     float* blt = beta ? beta + t : nullptr;
-    float* ut = w.u[t & 1];  // this step's u; the previous step's is w.u[(t + 1) & 1]
-    RsArgs ra{rup((B + 1) / 2, 8), L.Vp, T, fused ? t - 1 : -1, (flags & AA_DECODE_RS_SELF) ? 0 : RS_WAIT_TICKS,
-              w.u[(t + 1) & 1], w.summ, p.mlp_w, p.mlp_b, kt - B, ids};
-    const bool self = (flags & AA_DECODE_AT_SELF) != 0;
-    AtArgs at{w.V, w.vwv, p.wh, alt, (int64_t)T * P, blt, T, ut, w.ub, w.unorm, w.arr + (size_t)t * MT,
-              w.done + (size_t)t * B, self ? 0 : AT_WAIT_TICKS, self ? 0 : AT_GRACE_TICKS};
+    RsArgs ra{rup((B + 1) / 2, 8), L.Vp, T, t - 1, (flags & AA_DECODE_RS_SELF) ? 0 : RS_WAIT_TICKS, w.u, w.summ,
+              p.mlp_w, p.mlp_b, kt - B, ids};
     lstm_launch(L, p, B, tok, tok_ld, w.xg, w.hsp[cur], w.c[cur], w.h[nxt], w.hsp[nxt], w.c[nxt], w.s, w.part, s,
-                nullptr, fat || (fused && t > 0) ? &ra : nullptr, trace ? trace->lstm_events : nullptr, 2 * t,
-                fat ? &at : nullptr);
-    if (!fat)
-      atten_launch(L, p, B, w.V, w.vwv, w.h[nxt], w.s, w.part, ut, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
-                   alt, (int64_t)T * P, blt, T, s, 1, nullptr, trace ? trace->atten_events : nullptr, 2 * t);
+                nullptr, fused && t > 0 ? &ra : nullptr, trace ? trace->lstm_events : nullptr, 2 * t);
+    atten_launch(L, p, B, w.V, w.vwv, w.h[nxt], w.s, w.part, w.u, exact ? nullptr : w.ub, exact ? nullptr : w.unorm,
+                 alt, (int64_t)T * P, blt, T, s, 1, nullptr, trace ? trace->atten_events : nullptr, 2 * t);
     aa_event_t* sev = trace ? trace->screen_events : nullptr;
     aa_event_t* rev = trace ? trace->rescore_events : nullptr;
     if (exact) {
       AA_TLAUNCH(sev, 2 * t, k_vocab, dim3(MT * (L.Vp / 64)), dim3(256), 0, s, B, L.H, L.V, L.Vp, L.V,
-                 (const float*)ut, p.mlp_w, p.mlp_b, (float*)nullptr, kt);
+                 (const float*)w.u, p.mlp_w, p.mlp_b, (float*)nullptr, kt);
       hipLaunchKernelGGL(k_key_ids, dim3((B + 255) / 256), dim3(256), 0, s, kt, B, ids + t, T);
       continue;
     }
@@ -3598,7 +3215,7 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
              L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                             \
              reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
 #define AA_RESCORE(H_)                                                                                          \
-  AA_TLAUNCH(rev, 2 * t, k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, (const float*)ut,             \
+  AA_TLAUNCH(rev, 2 * t, k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, (const float*)w.u,           \
              (const float4*)w.summ, p.mlp_w, p.mlp_b, kt, ids, T, t)
     switch (H) {
       case 256: if (wide) AA_SCREEN2(256); else AA_SCREEN(256); break;
@@ -3639,24 +3256,12 @@ static int greedy_impl(const aa_model* m, const float* feats, int32_t B, int32_t
   // keys [T][B] cleared: the exact vocab stage accumulates into them by atomicMax (k_vocab); the
   // fused rescoring publishes them as readiness-tagged granules (a nonzero key = ready, k_lstm<.., RS>).
   // (The split default writes every key it produces; step 0's k_lstm takes <start> itself.)
-  // The fused attention's row claims and arrival counters (after the keys) are cleared with them.
-  const bool clear = (flags & AA_DECODE_EXACT_VOCAB) || ((flags & AA_DECODE_SPLIT_RESCORE) == 0 && T > 1) ||
-                     fused_attention(L, flags);
-  const DecodeInit init{w.tok0, B, w.keys, sync_words(B, T)};
+  const bool clear = (flags & AA_DECODE_EXACT_VOCAB) || ((flags & AA_DECODE_SPLIT_RESCORE) == 0 && T > 1);
+  const DecodeInit init{w.tok0, B, w.keys, T * B};
   rc = encoder_launch(L, p, feats, B, w.a_g, w.V, w.vg, w.h[0], w.c[0], w.vwv, w.xg,
                       trace ? trace->encoder_events : nullptr, flags, s, aux, w.hsp[0], clear ? &init : nullptr);
   if (rc) return rc;
   return decode_rows(L, p, w, B, T, flags, ids, alpha, beta, trace, s);
-}
-
-int aa_decode_launch_structure(const aa_dims* d, int32_t flags) {
-  const int rc = aa_check_dims(d);
-  if (rc != AA_OK) return rc;
-  const Layout L = make_layout(*d);
-  int r = 0;
-  if (!(flags & (AA_DECODE_EXACT_VOCAB | AA_DECODE_SPLIT_RESCORE))) r |= AA_LAUNCH_RESCORE_IN_LSTM;
-  if (fused_attention(L, flags)) r |= AA_LAUNCH_ATTEN_IN_LSTM;
-  return r;
 }
 
 int aa_greedy_decode(const aa_model* m, const float* feats, int32_t B, int32_t T, int64_t* ids, float* alpha,

@@ -510,8 +510,6 @@ def main():
     if depth > 1:
         pipelined(max(args.warmup, 2 * depth + 1, 4 * K))
     kern = ("lstm", "atten", "screen", "rescore")
-    structure = _lib.load().aa_decode_launch_structure(model._c_dims(), model._decode_flags())
-    atten_fused = bool(structure & _lib.LAUNCH_ATTEN_IN_LSTM)
     traces = []
     if not args.no_trace:
         for _ in range(K):
@@ -568,8 +566,7 @@ def main():
             lstm = ev["lstm"].pair_durations_ms()
             per["k_lstm(step0)"].append(lstm[0])  # step 0: GEMM + cell, no previous step to rescore
             per["k_lstm"] += lstm[1:]             # steps 1..T-1: + the rescoring of step t-1
-            if not atten_fused:  # (fused: the attention runs inside the k_lstm launch; no k_atten events)
-                per["k_atten"] += ev["atten"].pair_durations_ms()
+            per["k_atten"] += ev["atten"].pair_durations_ms()
             per["k_vscreen"] += ev["screen"].pair_durations_ms()
             # only the last step's rescoring has its own launch
             per["k_vrescore"].append(ev["rescore"].elapsed_ms(2 * T - 2, 2 * T - 1))
@@ -607,17 +604,6 @@ def main():
                               "note": entry["note"] + "; the launch also rescores step t-1's vocabulary "
                                       "candidates exactly (rescore_bytes_per_launch at HBM peak): "
                                       "frac_incl_rescoring = (FLOPs / peak + bytes / 8 TB/s) / duration"})
-                if atten_fused:
-                    ab = (atten_bytes_per_row() - v_restream_bytes_per_row()) * B
-                    vb = v_restream_bytes_per_row() * B
-                    ideal_all = ideal + ab / PEAK_HBM
-                    entry.update({"atten_bytes_per_launch": ab, "v_restream_bytes_per_launch": vb,
-                                  "ideal_us_fused": ideal_all * 1e6, "frac_fused": ideal_all / sec,
-                                  "ideal_us_fused_with_v_restream": (ideal_all + vb / PEAK_HBM) * 1e6,
-                                  "frac_fused_with_v_restream": (ideal_all + vb / PEAK_HBM) / sec,
-                                  "note": entry["note"] + "; AND the step's attention (k_lstm<512, .., AT>: the "
-                                          "attention's HBM-algorithmic bytes at HBM peak in frac_fused, plus its "
-                                          "per-step V re-read in frac_fused_with_v_restream)"})
             kernels[k] = entry
         kernel_sum = sum(e["ms_per_step"] for e in kernels.values())
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
@@ -641,17 +627,10 @@ def main():
                                        "the timestamps rocprofv3's kernel trace reads; no event packet between "
                                        "the launches); rocprofv3 summary of the same region: profiles/"}
         for key in ("algorithmic_flops_per_launch", "algorithmic_bytes_per_launch", "rescore_bytes_per_launch",
-                    "ideal_us_incl_rescoring", "frac_incl_rescoring", "atten_bytes_per_launch",
-                    "v_restream_bytes_per_launch", "ideal_us_fused", "frac_fused", "ideal_us_fused_with_v_restream",
-                    "frac_fused_with_v_restream"):
+                    "ideal_us_incl_rescoring", "frac_incl_rescoring"):
             if key in kd:
                 roofline[key] = kd[key]
-        if dominant == "k_lstm" and atten_fused:
-            roofline["note"] = ("steps 0..T-1: one launch runs h W_hh^T + the cell + the attention projections (the "
-                                "FLOPs priced in `frac`), the step's attention (its bytes priced in `frac_fused`) "
-                                "and, steps >= 1, the exact rescoring of the previous step's vocabulary candidates "
-                                "(bytes in `frac_incl_rescoring` / `frac_fused`); all at their own peaks, summed")
-        elif dominant == "k_lstm":
+        if dominant == "k_lstm":
             roofline["note"] = ("steps 1..T-1: one launch runs h W_hh^T + the cell + the attention projections (the "
                                 "FLOPs priced in `frac`) AND the exact rescoring of the previous step's vocabulary "
                                 "candidates (priced in `frac_incl_rescoring` at HBM peak); the step-0 launch "

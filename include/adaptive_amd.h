@@ -190,19 +190,6 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 #define AA_DECODE_RS_SELF 2048 /* test hook: the LSTM workgroups do not wait for the rescoring workgroups
                                   of their launch but rescore every row not yet published themselves
                                   (the fallback that keeps the fused launch deadlock-free); same ids */
-#define AA_DECODE_SPLIT_ATTEN 4096 /* the attention in its own launch per step (k_atten5) instead of inside
-                                      the step's LSTM launch (hidden 512); the same bits (cross-check path) */
-#define AA_DECODE_AT_SELF 8192 /* test hook: the fused launch's attention workgroups do not wait for their
-                                  row block; each row block's last LSTM workgroup computes every row not
-                                  yet claimed (the fallback that keeps the fused launch deadlock-free) */
-
-/* Launch structure of a greedy decode with these dims and flags (bit mask, or an AA_ERR_* code):
- * AA_LAUNCH_RESCORE_IN_LSTM: step t-1's exact rescoring runs inside step t's LSTM launch (the last
- * step's in k_vrescore); AA_LAUNCH_ATTEN_IN_LSTM: step t's attention runs inside step t's LSTM launch
- * (no k_atten launch: aa_trace.atten_events stay unrecorded, lstm_events time the fused launch). */
-#define AA_LAUNCH_RESCORE_IN_LSTM 1
-#define AA_LAUNCH_ATTEN_IN_LSTM 2
-AA_API int aa_decode_launch_structure(const aa_dims* dims, int32_t flags);
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];

@@ -303,20 +303,15 @@ def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device)
 
 @pytest.mark.parametrize("B,T", [(512, 20), (300, 9), (67, 5), (1, 4), (3, 2), (130, 1)])
 def test_fused_rescoring_equals_split(B, T, gpu_device):
-    """Step t-1's rescoring and step t's attention inside step t's LSTM launch (the default) == the
-    attention in its own launch (AA_DECODE_SPLIT_ATTEN) == the rescoring in its own launch too
-    (AA_DECODE_SPLIT_RESCORE) == the no-wait fallbacks that keep the fused launch deadlock-free: the
-    LSTM workgroups rescoring every unpublished row themselves (AA_DECODE_RS_SELF) and each row block's
-    last LSTM workgroup computing every unclaimed attention row (AA_DECODE_AT_SELF): ids, alpha and
-    beta bit for bit, on odd and single-row batches and T = 1."""
+    """Step t-1's rescoring inside step t's LSTM launch (the default) == its own launch per step
+    (AA_DECODE_SPLIT_RESCORE) == the LSTM workgroups rescoring every unpublished row themselves
+    (AA_DECODE_RS_SELF, the no-wait fallback that keeps the fused launch deadlock-free): ids, alpha
+    and beta bit for bit, on odd and single-row batches and T = 1 (no fused launch)."""
     from adaptive_amd import _lib
     m = _model(99, 0.02)
     feats = torch.from_numpy(synth.make_features(B, seed=B + T)).to(gpu_device)
     a = m.sampler(feats, max_len=T)
-    assert _lib.load().aa_decode_launch_structure(m._c_dims(), 0) == (_lib.LAUNCH_RESCORE_IN_LSTM
-                                                                      | _lib.LAUNCH_ATTEN_IN_LSTM)
-    for extra in (_lib.DECODE_SPLIT_ATTEN, _lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF, _lib.DECODE_AT_SELF,
-                  _lib.DECODE_AT_SELF | _lib.DECODE_RS_SELF):
+    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF):
         m.decode_extra_flags = extra
         b = m.sampler(feats, max_len=T)
         m.decode_extra_flags = 0
