@@ -865,7 +865,15 @@ __global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, 
 // (Atten.affine_g / affine_s, adaptive_attention.py:35,45): part[b][tile][j] = sum_{u in tile}
 // (j < 49 ? h'_u W_g[j][u] : s_u W_s[j-49][u]); k_atten adds the H/16 partials in tile order.
 // ---------------------------------------------------------------------------------------------
-constexpr int PART = 128;  // partial-projection row pitch (2 x 49 used)
+constexpr int PART = 128;  // partial-projection row pitch (AA_PART_ALIGN: W_g h outputs at 0..48, W_s s at 64..112)
+// Column of projection output j (0..97: W_g then W_s) in a partial row.  AA_PART_ALIGN: each half
+// starts on a 256-B boundary, so every store instruction of the tile's projection phase (a 32 x 32
+// accumulator block: two rows x 32 columns) writes two whole 128-B lines (the write-through stores of
+// partial lines otherwise cost the memory side a read-modify-write each).
+#ifndef AA_PART_ALIGN
+#define AA_PART_ALIGN 1
+#endif
+__device__ __forceinline__ int part_col(int j) { return AA_PART_ALIGN ? (j < P ? j : 64 + (j - P)) : j; }
 
 // The GEMM h_{t-1} W_hh^T runs on bf16 MFMA with 3-way split operands (see k_enc_v3): h arrives
 // already split (hsp_in, written by the previous step's epilogue or k_split_rows) and W_hh is
@@ -984,11 +992,14 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
       const float wv = jj < P ? Wsl[u * WSP + jgc] : 0.f;
       pacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv, pacc, 0, 0, 0);
     }
-    if (jj < P) {
+    // (AA_PART_ALIGN: all 32 lanes store -- columns jj >= P hold zeros, their W values being 0 -- so the
+    // lines are whole)
+    const int col = AA_PART_ALIGN ? (cb < 2 ? 0 : 64) + jj : jg;
+    if (AA_PART_ALIGN || jj < P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mr = m0 + rb * 32 + acc_row(r, lane);
-        if (mr < B) st_wt<1>(&part[((int64_t)mr * NTn + nt) * PART + jg], pacc[r]);
+        if (mr < B) st_wt<1>(&part[((int64_t)mr * NTn + nt) * PART + col], pacc[r]);
       }
     }
   }
@@ -1443,7 +1454,7 @@ __global__ __launch_bounds__(256) void k_atten(int B, int NTL, int kdiv, const f
   //  for partials + VWv, while the 98 V values of this thread stay in flight.)  No branches
   //  around loads: out-of-range lanes read clamped addresses and their values are never used.
   constexpr int NT16 = H / 16;  // == NTL
-  const int tp = t < 2 * P ? t : 2 * P - 1;
+  const int tp = part_col(t < 2 * P ? t : 2 * P - 1);
   float pv[NT16];
   {
     const float* pp = part + (int64_t)b * NT16 * PART + tp;
@@ -1701,7 +1712,7 @@ __global__ __launch_bounds__(512) void k_atten5(int B, int kdiv, const float* __
   const int b = blockIdx.x;
   const int img = kdiv == 1 ? b : b / kdiv;
   // loads, oldest first in the order they are consumed; clamped addresses, no branches
-  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
+  const int grp = t >> 7, jp = t & 127, jpc = part_col(jp < 2 * P ? jp : 2 * P - 1);
   float pv[NG];
   {
     const float* pp = part + ((int64_t)b * NT16 + grp) * PART + jpc;
@@ -1768,7 +1779,7 @@ __global__ __launch_bounds__(512) void k_atten5b(const float* __restrict__ h_new
   __shared__ float sh_norm[KB][16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int img = blockIdx.x, r0 = img * KB;
-  const int grp = t >> 7, jp = t & 127, jpc = jp < 2 * P ? jp : 2 * P - 1;
+  const int grp = t >> 7, jp = t & 127, jpc = part_col(jp < 2 * P ? jp : 2 * P - 1);
   float pv[KB][NG];
 #pragma unroll
   for (int r = 0; r < KB; ++r) {
