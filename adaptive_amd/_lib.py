@@ -23,6 +23,7 @@ DECODE_FP32_ENCODER = 2
 DECODE_ONE_STREAM = 512
 DECODE_SPLIT_RESCORE = 1024  # rescoring in its own launch per step (cross-check of the fused default)
 DECODE_RS_SELF = 2048  # test hook: fused launch's LSTM workgroups rescore unpublished rows themselves
+DECODE_SCREEN4 = 4096  # vocab screen on k_vscreen2 (4 waves) instead of k_vscreen8: the same summaries
 BEAM_FAST = 256
 TRAIN_BF16 = 128
 MAX_BEAM = 8

@@ -2345,6 +2345,116 @@ __global__ __launch_bounds__(256, AA_SCREEN_OCC) void k_vscreen2(int B, int V, i
   AA_TS(2, 2);
 }
 
+// The wide screen on 512 threads (k_vscreen8, the default): the same 128 x 160 tile, W stages and
+// per-block products, but two waves per row block -- wave w < 4 takes column blocks 0..2 of rows
+// 32 w.., wave w + 4 blocks 3..4 of the same rows -- so each SIMD holds two waves (one of each group)
+// whose MFMA chains and LDS reads interleave, where k_vscreen2's single wave per SIMD waited on every
+// LDS read (41 % of wave cycles waiting).  Every block accumulates its chunks in the
+// same order, so the summaries are k_vscreen2's bit for bit.
+constexpr int SC8_NT = 512, SC8_NA = 3, SC8_NBB = SC2_NB - SC8_NA;  // threads; blocks of group 0 / 1
+template <int H, int NBW>
+__device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, const bf16x8* __restrict__ ua,
+                                             const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                             bf16x8 (*Ws)[SC2_STAGE], float2* un_s, floatx16 (&acc)[NBW],
+                                             const float4* __restrict__ gs, float4* gs_s) {
+  constexpr int KC = H / 16, NS = KC / SC2_KS, PER = (SC2_STAGE + SC8_NT - 1) / SC8_NT;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bf16x8* a0 = ua + (size_t)((m0 >> 5) + (wave & 3)) * KC * 64 + lane;
+  constexpr int AH = AA_SCREEN_AHEAD < NS ? AA_SCREEN_AHEAD : NS, RW = AH, RU = AH + 1;
+  bf16x8 fa[RU][SC2_KS];
+  auto uload = [&](int s, int slot) {
+#pragma unroll
+    for (int c = 0; c < SC2_KS; ++c) fa[slot][c] = a0[(size_t)(s * SC2_KS + c) * 64];
+  };
+  const bf16x8* wbase = wf + (size_t)(n0 >> 5) * KC * 64;
+  bf16x8 wr[RW][PER];
+  auto gload = [&](int s, int slot) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = t + SC8_NT * i;
+      if (PER * SC8_NT == SC2_STAGE || j < SC2_STAGE) {  // (wave-uniform)
+        const int b = j / (SC2_KS * 64), r = j - b * (SC2_KS * 64);
+        wr[slot][i] = wbase[((size_t)b * KC + s * SC2_KS) * 64 + r];
+      }
+    }
+  };
+  auto lstore = [&](int buf, int slot) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = t + SC8_NT * i;
+      if (PER * SC8_NT == SC2_STAGE || j < SC2_STAGE) Ws[buf][j] = wr[slot][i];
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < AH; ++s) uload(s, s);
+#pragma unroll
+  for (int b = 0; b < NBW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < AH; ++s) gload(s, s);
+  if (t < SC2_BM) {
+    const int r = m0 + t;
+    un_s[t] = make_float2(unorm[r < B ? r : B - 1], unorm[B + (r < B ? r : B - 1)]);
+  } else if (t < SC2_BM + SC2_NB) {
+    gs_s[t - SC2_BM] = gs[n0 / VS_TILE + t - SC2_BM];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    lstore(s & 1, s % RW);
+    if (s + AH < NS) {
+      gload(s + AH, s % RW);
+      uload(s + AH, (s + AH) % RU);
+    }
+    __syncthreads();
+    const bf16x8* ws = Ws[s & 1] + lane;
+#pragma unroll
+    for (int c = 0; c < SC2_KS; ++c) {
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) {
+        const bf16x8 w = ws[((b0 + b) * SC2_KS + c) * 64];
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s % RU][c], w, acc[b], 0, 0, 0);
+      }
+    }
+  }
+}
+template <int H, int NBW>
+__device__ __forceinline__ void screen8_group(int B, int V, int m0, int n0, int b0, int NTn,
+                                              const bf16x8* __restrict__ ua, const float* __restrict__ unorm,
+                                              const bf16x8* __restrict__ wf, const float4* __restrict__ gs,
+                                              const float* __restrict__ bias, float4* __restrict__ summ,
+                                              bf16x8 (*Ws)[SC2_STAGE], float2* un_s, float4* gs_s) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31;
+  float bvs[NBW];
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) bvs[b] = bias[n0 + 32 * (b0 + b) + li];
+  floatx16 acc[NBW];
+  screen8_main<H, NBW>(B, m0, n0, b0, ua, unorm, wf, Ws, un_s, acc, gs, gs_s);
+  AA_TS(2, 1);
+  const int row0 = m0 + 32 * (wave & 3);
+  screen_blocks_summ<H, NBW>(acc, row0, n0 / VS_TILE + b0, bvs, gs_s + b0, un_s + 32 * (wave & 3), n0 + 32 * b0, V, B,
+                             NTn, summ);
+}
+template <int H>
+__global__ __launch_bounds__(SC8_NT) void k_vscreen8(int B, int V, int Vp, const bf16x8* __restrict__ ua,
+                                                     const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
+                                                     const float4* __restrict__ gs, const float* __restrict__ bias,
+                                                     float4* __restrict__ summ) {
+  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
+  __shared__ float2 un_s[SC2_BM];
+  __shared__ float4 gs_s[SC2_NB];
+  AA_TS(2, 0);
+  const int NTn = Vp / VS_TILE, NT = Vp / SC2_BN, MT = (B + SC2_BM - 1) / SC2_BM;
+  const int L = xcd_remap(blockIdx.x, MT * NT);
+  const int nt = L / MT, mt = L % MT;  // m fastest: a W tile is shared inside an XCD
+  const int m0 = mt * SC2_BM, n0 = nt * SC2_BN;
+  if (threadIdx.x < 256)  // (wave-uniform) column blocks 0..2
+    screen8_group<H, SC8_NA>(B, V, m0, n0, 0, NTn, ua, unorm, wf, gs, bias, summ, Ws, un_s, gs_s);
+  else                    // column blocks 3..4
+    screen8_group<H, SC8_NBB>(B, V, m0, n0, SC8_NA, NTn, ua, unorm, wf, gs, bias, summ, Ws, un_s, gs_s);
+  AA_TS(2, 2);
+}
+
 // Exact fp32 logit of one column, computed by a group of 8 lanes (lane8 = 0..7): lane8 j runs the
 // fma chain of partial j (K-steps [j*per, (j+1)*per) of 32, in the MFMA k order: pairs (s, 16+s)),
 // then the fixed tree ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) over xor-1/2/4 shuffles, then + bias.
@@ -3221,10 +3331,20 @@ static int decode_rows(const Layout& L, const MP& p, const DecodeWS& w, int B, i
   AA_TLAUNCH(sev, 2 * t, k_vscreen<H_>, dim3(((B + SC_BM - 1) / SC_BM) * (L.Vp / SC_BN)), dim3(256), 0, s, B, L.V, \
              L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                                  \
              reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
+#ifndef AA_SCREEN8
+#define AA_SCREEN8 1
+#endif
 #define AA_SCREEN2(H_)                                                                                          \
-  AA_TLAUNCH(sev, 2 * t, k_vscreen2<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, B, \
-             L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                             \
-             reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ)
+  do {                                                                                                         \
+    if (AA_SCREEN8 && !(flags & AA_DECODE_SCREEN4))                                                            \
+      AA_TLAUNCH(sev, 2 * t, k_vscreen8<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(SC8_NT), 0, \
+                 s, B, L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                \
+                 reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ);                        \
+    else                                                                                                       \
+      AA_TLAUNCH(sev, 2 * t, k_vscreen2<H_>, dim3(((B + SC2_BM - 1) / SC2_BM) * (L.Vp / SC2_BN)), dim3(256), 0, s, \
+                 B, L.V, L.Vp, reinterpret_cast<const bf16x8*>(w.ub), (const float*)w.unorm,                   \
+                 reinterpret_cast<const bf16x8*>(p.mlp_wb), p.mlp_gs, p.mlp_b, w.summ);                        \
+  } while (0)
 #define AA_RESCORE(H_)                                                                                          \
   AA_TLAUNCH(rev, 2 * t, k_vrescore<H_>, dim3(B), dim3(RS_NT), 0, s, B, L.V, L.Vp, (const float*)w.u,           \
              (const float4*)w.summ, p.mlp_w, p.mlp_b, kt, ids, T, t)

@@ -190,6 +190,8 @@ AA_API size_t aa_decode_workspace_bytes(const aa_dims* dims, int32_t B, int32_t 
 #define AA_DECODE_RS_SELF 2048 /* test hook: the LSTM workgroups do not wait for the rescoring workgroups
                                   of their launch but rescore every row not yet published themselves
                                   (the fallback that keeps the fused launch deadlock-free); same ids */
+#define AA_DECODE_SCREEN4 4096 /* the vocab screen on four waves per 128 x 160 tile (k_vscreen2) instead
+                                  of eight (k_vscreen8); the same summaries bit for bit (cross-check) */
 
 /* Whole greedy decode = Encoder2Decoder.sampler(images, max_len=T) (adaptive_attention.py:168-216,
  * with the baseline's states transpose, baseline_attention.py:251-252).  feats [B,C,7,7];

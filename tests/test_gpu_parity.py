@@ -305,13 +305,14 @@ def test_screened_vocab_equals_exact_vocab(seed, noise, fseed, B, T, gpu_device)
 def test_fused_rescoring_equals_split(B, T, gpu_device):
     """Step t-1's rescoring inside step t's LSTM launch (the default) == its own launch per step
     (AA_DECODE_SPLIT_RESCORE) == the LSTM workgroups rescoring every unpublished row themselves
-    (AA_DECODE_RS_SELF, the no-wait fallback that keeps the fused launch deadlock-free): ids, alpha
-    and beta bit for bit, on odd and single-row batches and T = 1 (no fused launch)."""
+    (AA_DECODE_RS_SELF, the no-wait fallback that keeps the fused launch deadlock-free) == the screen on
+    four waves per tile (AA_DECODE_SCREEN4, k_vscreen2 instead of k_vscreen8): ids, alpha and beta bit
+    for bit, on odd and single-row batches and T = 1 (no fused launch)."""
     from adaptive_amd import _lib
     m = _model(99, 0.02)
     feats = torch.from_numpy(synth.make_features(B, seed=B + T)).to(gpu_device)
     a = m.sampler(feats, max_len=T)
-    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF):
+    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF, _lib.DECODE_SCREEN4):
         m.decode_extra_flags = extra
         b = m.sampler(feats, max_len=T)
         m.decode_extra_flags = 0
@@ -333,7 +334,7 @@ def test_fused_rescoring_nan_vocab_weights(gpu_device):
     feats = torch.from_numpy(synth.make_features(67, seed=8)).to(gpu_device)
     a = m.sampler(feats, max_len=4)
     assert bool(((a[0] >= 0) & (a[0] < m.dims.vocab)).all())
-    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF):
+    for extra in (_lib.DECODE_SPLIT_RESCORE, _lib.DECODE_RS_SELF, _lib.DECODE_SCREEN4):
         m.decode_extra_flags = extra
         b = m.sampler(feats, max_len=4)
         m.decode_extra_flags = 0
