@@ -2360,7 +2360,10 @@ __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, cons
   constexpr int KC = H / 16, NS = KC / SC2_KS, PER = (SC2_STAGE + SC8_NT - 1) / SC8_NT;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const bf16x8* a0 = ua + (size_t)((m0 >> 5) + (wave & 3)) * KC * 64 + lane;
-  constexpr int AH = AA_SCREEN_AHEAD < NS ? AA_SCREEN_AHEAD : NS, RW = AH, RU = AH + 1;
+#ifndef AA_SCREEN8_AHEAD
+#define AA_SCREEN8_AHEAD 2
+#endif
+  constexpr int AH = AA_SCREEN8_AHEAD < NS ? AA_SCREEN8_AHEAD : NS, RW = AH, RU = AH + 1;
   bf16x8 fa[RU][SC2_KS];
   auto uload = [&](int s, int slot) {
 #pragma unroll
