@@ -65,8 +65,13 @@ class Adam(torch.optim.Optimizer):
             # from (the caching allocator hands back the same gradient blocks step after step): the
             # per-tensor checks and the table build then cost nothing per step
             state = self.state
-            ident = tuple((id(p), id(p.grad), p.data_ptr(), p.grad.data_ptr(),
-                           *(id(x) for x in state[p].values())) if p in state else (id(p),) for p in live)
+            # the plan (validated tensors, launch tables) is reused while every parameter, its state
+            # tensors and its gradient's storage are the ones it was built for: gradient tensors are new
+            # objects every step (zero_grad sets them to None), but the caching allocator hands the same
+            # blocks back, so the key holds their data pointers and layouts, not their ids
+            ident = tuple((id(p), p.data_ptr(), p.grad.data_ptr(), p.grad.dtype, p.grad.shape, p.grad.stride(),
+                           p.grad.device, *(id(x) for x in state[p].values())) if p in state else (id(p),)
+                          for p in live)
             plan = self._tables.get(gi)
             if plan is None or plan[0] != ident:
                 plan = self._plan(live, ident)
