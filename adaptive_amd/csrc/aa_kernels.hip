@@ -1023,6 +1023,12 @@ __device__ __forceinline__ void lstm_cell_tail(int B, int m0, int nt, const floa
 constexpr int LS_NB = AA_LSTM_NB;             // ring stages (LS_NB - 1 in flight ahead of the one multiplied)
 constexpr int LS_STAGE = 24 * 64;             // bf16x8 per stage
 constexpr int LS_GATHERS = 12;                // ordinary loads issued by k_lstm's gathers (ISA-checked)
+// fragments each wave DMAs per ring stage (3; AA_RING_NPW = 2 is a timing-only probe that moves two
+// thirds of the bytes and computes garbage)
+#ifndef AA_RING_NPW
+#define AA_RING_NPW 3
+#endif
+constexpr int LS_NPW = AA_RING_NPW;
 
 // s_waitcnt vmcnt(n) for an n that is a compile-time constant once the caller's loop is unrolled
 template <int V>
@@ -1069,7 +1075,7 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
   auto issue = [&](int it) {
     bf16x8* dst = stg + (it % NB) * LS_STAGE + (3 * wave) * 64;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < LS_NPW; ++i)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)it * 3 * 64),
                                        (__attribute__((address_space(3))) void*)(dst + i * 64), 16, 0, 0);
   };
@@ -1093,7 +1099,7 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
   pre();  // waits for its own older loads with vmcnt(3 NB); issues exactly LS_GATHERS loads
   __builtin_amdgcn_sched_barrier(0);
   // stage 0 landed (younger: stages 1 .. NB-1 and the gathers)
-  vm_wait(3 * (NB - 1) + LS_GATHERS);
+  vm_wait(LS_NPW * (NB - 1) + LS_GATHERS);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   lread(0, 0);
 #pragma unroll
@@ -1103,7 +1109,7 @@ __device__ __forceinline__ void lstm_gemm_lds(const bf16x8* af0, const bf16x8* a
       // stage it + 1 landed: younger are the stages issued after it (up to it + NB - 1) and, while
       // it + 1 <= NB - 1, the gathers (issued after stage NB - 1)
       const int last = it + NB - 1 < N - 1 ? it + NB - 1 : N - 1;
-      int younger = 3 * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0);
+      int younger = LS_NPW * (last - (it + 1)) + (it + 1 <= NB - 1 ? LS_GATHERS : 0);
       if (JK >= 0 && it >= JG + 1 && it + 1 <= SG) younger += NG2;
       if (JK >= 0 && it >= JK + 1 && it + 1 <= SK && wave == 0) younger += 1;
       vm_wait(younger);
@@ -1360,7 +1366,7 @@ __global__ __launch_bounds__(512, AA_LSTM_OCC) void k_lstm(int B, int V, const i
   } else {
     lstm_gemm_lds<H>(af0, af1, wf0, wf1, reinterpret_cast<bf16x8*>(lds), Pt, [&] {
       // wave 0's token DMA is older than its ring DMAs: retire it, then every wave reads its row's
-      if (t < 64) vm_wait(3 * (LS_NB < H / 32 ? LS_NB : H / 32));
+      if (t < 64) vm_wait(LS_NPW * (LS_NB < H / 32 ? LS_NB : H / 32));
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       tk = tok ? tok_lds[rr] : 1;
       gathers();
