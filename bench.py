@@ -227,7 +227,7 @@ def path_ideal_seconds(B: int, T: int, Vp: int = 10240, v_restream: bool = True)
 # id / key initialisation, so k_split_rows and k_decode_init do not run
 def path_launches(T: int) -> dict:
     return {"k_enc_v4": 1, "k_gemm3": 3,
-            "k_lstm": T, "k_atten5": T, "k_vscreen2": T, "k_vrescore": 1}  # steps 0..T-2 rescored inside k_lstm
+            "k_lstm": T, "k_atten5": T, "k_vscreen8": T, "k_vrescore": 1}  # steps 0..T-2 rescored inside k_lstm
 
 
 def path_traffic(B: int, T: int, traffic_json: str) -> dict:
@@ -616,7 +616,7 @@ def main():
         pass
     if dominant:
         kd = kernels[dominant]
-        pmc_name = {"k_atten": "k_atten5", "k_vscreen": "k_vscreen2"}.get(dominant, dominant.split("(")[0])
+        pmc_name = {"k_atten": "k_atten5", "k_vscreen": "k_vscreen8"}.get(dominant, dominant.split("(")[0])
         traffic = traffic_all.get(pmc_name, {}).get("hbm_bytes_per_launch")
         roofline = {"kernel": dominant, "bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"],
                     "unit": kd["unit"], "frac": kd["frac"], "traffic": traffic,
@@ -698,7 +698,7 @@ def main():
                    + ("" if backend == "nccl" else f" ({backend} rehearsal)"),
                    "batches_in_flight": 1, "feature_buffers": nbuf,
                    "launch": "direct kernel launches from one C call per sampler() (no hipGraph, no per-buffer cache)",
-                   "vocab_stage": "k_vscreen2 (bf16 screen, granule summaries) + exact fp32 rescoring of the "
+                   "vocab_stage": "k_vscreen8 (bf16 screen, granule summaries) + exact fp32 rescoring of the "
                                   "candidates inside the next step's k_lstm launch (k_vrescore for the last step)",
                    "timed_step": "decode + (N > 1: all-gather of ids) + ids device->host copy",
                    "headline": "one sampler() call after another on resident batches"},

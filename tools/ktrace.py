@@ -24,7 +24,7 @@ KERNELS = {0: ("k_lstm (fused, GEMM role)", [(0, "entry"), (5, "ring done"), (1,
                                              (3, "cell stored"), (4, "exit")], 256),
            4: ("k_lstm (fused, rescoring role)", [(0, "entry"), (1, "key published")], 0),
            1: ("k_atten5", list(enumerate(["entry", "proj barrier", "scores barrier", "softmax barrier", "exit"])), 0),
-           2: ("k_vscreen2", list(enumerate(["entry", "mainloop done", "exit"])), 0),
+           2: ("k_vscreen8", list(enumerate(["entry", "mainloop done", "exit"])), 0),
            3: ("k_vrescore", list(enumerate(["entry", "M reduced", "candidates", "exit"])), 0)}
 
 
