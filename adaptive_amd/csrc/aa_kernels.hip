@@ -2358,6 +2358,9 @@ __global__ __launch_bounds__(256, AA_SCREEN_OCC) void k_vscreen2(int B, int V, i
 // LDS read (41 % of wave cycles waiting).  Every block accumulates its chunks in the
 // same order, so the summaries are k_vscreen2's bit for bit.
 constexpr int SC8_NT = 512, SC8_NA = 3, SC8_NBB = SC2_NB - SC8_NA;  // threads; blocks of group 0 / 1
+#ifndef AA_SCREEN8_RING3
+#define AA_SCREEN8_RING3 0
+#endif
 template <int H, int NBW>
 __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, const bf16x8* __restrict__ ua,
                                              const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
@@ -2408,6 +2411,30 @@ __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, cons
   } else if (t < SC2_BM + SC2_NB) {
     gs_s[t - SC2_BM] = gs[n0 / VS_TILE + t - SC2_BM];
   }
+#if AA_SCREEN8_RING3
+  // three LDS buffers: stage s + 1's W is stored in the middle of stage s's MFMAs (its buffer was last
+  // read in stage s - 2, before this stage's barrier), so the store's latency is off the
+  // barrier -> read -> MFMA path; one barrier per stage
+  lstore(0, 0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    __syncthreads();
+    if (s + AH < NS) {
+      gload(s + AH, (s + AH) % RW);
+      uload(s + AH, (s + AH) % RU);
+    }
+    const bf16x8* ws = Ws[s % 3] + lane;
+#pragma unroll
+    for (int c = 0; c < SC2_KS; ++c) {
+      if (c == SC2_KS / 2 && s + 1 < NS) lstore((s + 1) % 3, (s + 1) % RW);
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) {
+        const bf16x8 w = ws[((b0 + b) * SC2_KS + c) * 64];
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s % RU][c], w, acc[b], 0, 0, 0);
+      }
+    }
+  }
+#else
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     lstore(s & 1, s % RW);
@@ -2426,6 +2453,7 @@ __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, cons
       }
     }
   }
+#endif
 }
 template <int H, int NBW>
 __device__ __forceinline__ void screen8_group(int B, int V, int m0, int n0, int b0, int NTn,
@@ -2449,7 +2477,7 @@ __global__ __launch_bounds__(SC8_NT) void k_vscreen8(int B, int V, int Vp, const
                                                      const float* __restrict__ unorm, const bf16x8* __restrict__ wf,
                                                      const float4* __restrict__ gs, const float* __restrict__ bias,
                                                      float4* __restrict__ summ) {
-  __shared__ __attribute__((aligned(16))) bf16x8 Ws[2][SC2_STAGE];
+  __shared__ __attribute__((aligned(16))) bf16x8 Ws[AA_SCREEN8_RING3 ? 3 : 2][SC2_STAGE];
   __shared__ float2 un_s[SC2_BM];
   __shared__ float4 gs_s[SC2_NB];
   AA_TS(2, 0);
