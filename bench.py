@@ -746,6 +746,12 @@ def main():
                                   "figures"},
         "kernels": kernels,
         "traced_ms_per_step": None if traced_elapsed is None else 1e3 * traced_elapsed / K,
+        "traced_note": "the per-kernel figures (kernels, roofline) come from a SEPARATE region of the same K steps "
+                       "in which every launch carries a hipExtLaunchKernel start / stop event pair; that region "
+                       "runs slower than the timed region (traced_ms_per_step vs ms_per_step: the event packets "
+                       "add time between launches), while each kernel's own duration is the dispatch's begin / end "
+                       "and agrees with rocprofv3's kernel trace (profiles/); `value` and `ms_per_step` are from "
+                       "the uninstrumented regions",
         "kernel_sum_ms_per_step": kernel_sum if kernels else None,
         "kernel_sum_note": "sum over the kernels of median duration x launches per step (the encoder's heads / x_g "
                            "run on the aux stream beside the VWv GEMM, so they may overlap) against ms_per_step; "
