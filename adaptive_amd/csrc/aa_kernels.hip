@@ -2359,7 +2359,7 @@ __global__ __launch_bounds__(256, AA_SCREEN_OCC) void k_vscreen2(int B, int V, i
 // same order, so the summaries are k_vscreen2's bit for bit.
 constexpr int SC8_NT = 512, SC8_NA = 3, SC8_NBB = SC2_NB - SC8_NA;  // threads; blocks of group 0 / 1
 #ifndef AA_SCREEN8_RING3
-#define AA_SCREEN8_RING3 0
+#define AA_SCREEN8_RING3 1
 #endif
 template <int H, int NBW>
 __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, const bf16x8* __restrict__ ua,
@@ -2412,9 +2412,10 @@ __device__ __forceinline__ void screen8_main(int B, int m0, int n0, int b0, cons
     gs_s[t - SC2_BM] = gs[n0 / VS_TILE + t - SC2_BM];
   }
 #if AA_SCREEN8_RING3
-  // three LDS buffers: stage s + 1's W is stored in the middle of stage s's MFMAs (its buffer was last
-  // read in stage s - 2, before this stage's barrier), so the store's latency is off the
-  // barrier -> read -> MFMA path; one barrier per stage
+  // three LDS buffers (the default): stage s + 1's W is stored in the middle of stage s's MFMAs (its
+  // buffer was last read in stage s - 2, before this stage's barrier), so the store's latency is off
+  // the barrier -> read -> MFMA path; one barrier per stage.  10.1 -> 9.7 us, sequential decode
+  // +0.7 % (A/B, profiles/r06i_screen_ring3_ab.txt); four stages ahead of the W / u loads: no gain
   lstore(0, 0);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
