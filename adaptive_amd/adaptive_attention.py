@@ -335,6 +335,18 @@ class Encoder2Decoder(nn.Module):
             raise ValueError(f"trunk output {tuple(A.shape)} is not [B,{self.dims.channels},7,7] (images must be 224x224)")
         return A.contiguous()
 
+    def _ref_params(self) -> list:
+        """The 21 reference parameters in aa_ref_weights order, looked up through the modules'
+        parameter dicts on every call (so a replaced Parameter is seen) -- a few dict lookups per
+        parameter instead of named_parameters()'s walk over every module (≈0.07 ms per training step)."""
+        out = []
+        for mods, name in _WEIGHT_PATHS:
+            m = self
+            for a in mods:
+                m = m._modules[a]
+            out.append(m._parameters[name])
+        return out
+
     def _c_dims(self) -> _lib.Dims:
         d = self.dims
         return _lib.Dims(d.embed, d.hidden, d.vocab, d.channels, d.spatial)
@@ -706,9 +718,7 @@ class Encoder2Decoder(nn.Module):
         if T > captions.size(1):
             raise ValueError("lengths exceed the caption width")
         caps = captions.to(device=dev, dtype=torch.int64).contiguous()
-        named = dict(self.named_parameters())
-        params = [named[k] for _, k in _lib.WEIGHT_FIELDS]
-        data = _TeacherForced.apply(self, images, caps, len_dev, N, T, *params)
+        data = _TeacherForced.apply(self, images, caps, len_dev, N, T, *self._ref_params())
         return PackedSequence(data, batch_sizes.clone())
 
 
@@ -725,6 +735,9 @@ def packed_batch_sizes(lengths) -> list:
     for t in range(lengths[0] - 2, -1, -1):
         bs[t] += bs[t + 1]
     return bs
+
+
+_WEIGHT_PATHS = [(tuple(k.split(".")[:-1]), k.split(".")[-1]) for _, k in _lib.WEIGHT_FIELDS]
 
 
 class _TeacherForced(torch.autograd.Function):

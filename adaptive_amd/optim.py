@@ -65,20 +65,25 @@ class Adam(torch.optim.Optimizer):
             # from (the caching allocator hands back the same gradient blocks step after step): the
             # per-tensor checks and the table build then cost nothing per step
             state = self.state
-            # the plan (validated tensors, launch tables) is reused while every parameter, its state
-            # tensors and its gradient's storage are the ones it was built for: gradient tensors are new
-            # objects every step (zero_grad sets them to None), but the caching allocator hands the same
-            # blocks back, so the key holds their data pointers and layouts, not their ids
-            ident = tuple((id(p), p.data_ptr(), p.grad.data_ptr(), p.grad.dtype, p.grad.shape, p.grad.stride(),
-                           p.grad.device, *(id(x) for x in state[p].values())) if p in state else (id(p),)
-                          for p in live)
+            # the plan (validated parameters, their state, the launch tables) is reused while the
+            # parameters and their state tensors are the same objects (load_state_dict replaces the
+            # state: rebuilt); the gradients are new tensors every step (zero_grad sets them to None,
+            # and the caching allocator need not hand back the same blocks), so they are checked and
+            # their pointers written into the tables on every step
+            ident = tuple((id(p), *(id(x) for x in state[p].values())) if p in state else (id(p),) for p in live)
             plan = self._tables.get(gi)
             if plan is None or plan[0] != ident:
                 plan = self._plan(live, ident)
                 if len(self._tables) > 16:
                     self._tables.clear()
                 self._tables[gi] = plan
-            _, steps, calls = plan
+            for p, (arr, i) in zip(live, plan[3]):
+                g = p.grad
+                if g.dtype is not torch.float32 or g.is_sparse or not g.is_cuda or not g.is_contiguous() \
+                        or g.shape != p.shape or g.device != p.device:
+                    self._check_grad(p)
+                arr[i].grad = g.data_ptr()
+            _, steps, calls, _ = plan
             # the step counts, as torch.optim.Adam keeps them (CPU float32 tensors), one foreach add
             torch._foreach_add_(steps, 1.0)
             for dev, first, arr, n in calls:
@@ -94,14 +99,7 @@ class Adam(torch.optim.Optimizer):
         count for an update that never ran: torch's bias correction would drift), create missing
         state, and group the tensors that share a device and a step count into launch tables."""
         for p in live:
-            if p.grad.is_sparse:
-                raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
-            _require_hip(p, "parameter")
-            _require_hip(p.grad, "gradient")
-            if not (p.is_contiguous() and p.grad.is_contiguous()):
-                raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
-            if p.grad.shape != p.shape or p.grad.device != p.device:
-                raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
+            self._check_grad(p)
         steps, by_step = [], {}
         for i, p in enumerate(live):
             st = self.state[p]
@@ -113,11 +111,24 @@ class Adam(torch.optim.Optimizer):
             by_step.setdefault((p.device, float(st["step"].item())), []).append(
                 (i, (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                      p.numel())))
-        calls = []
+        calls, gslots = [], [None] * len(live)
         for (dev, _), rows in by_step.items():
             arr = (_lib.AdamTensor * len(rows))(*[_lib.AdamTensor(*r) for _, r in rows])
             calls.append((dev, rows[0][0], arr, len(rows)))
-        return ident, steps, calls
+            for j, (i, _) in enumerate(rows):
+                gslots[i] = (arr, j)
+        return ident, steps, calls, gslots
+
+    @staticmethod
+    def _check_grad(p):
+        if p.grad.is_sparse:
+            raise RuntimeError("adaptive_amd.optim.Adam does not support sparse gradients")
+        _require_hip(p, "parameter")
+        _require_hip(p.grad, "gradient")
+        if not (p.is_contiguous() and p.grad.is_contiguous()):
+            raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
+        if p.grad.shape != p.shape or p.grad.device != p.device:
+            raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
 
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
