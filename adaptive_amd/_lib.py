@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
@@ -78,6 +78,13 @@ class AdamTensor(Structure):
 ADAM_MAX_TENSORS = 24
 
 
+class GradTensor(Structure):
+    _fields_ = [("grad", c_void_p), ("numel", c_int64)]
+
+
+CLIP_MAX_TENSORS = 24
+
+
 class Trace(Structure):
     _fields_ = [("encoder_events", c_void_p), ("lstm_events", c_void_p), ("atten_events", c_void_p),
                 ("screen_events", c_void_p), ("rescore_events", c_void_p), ("gemm_events", c_void_p)]
@@ -133,6 +140,8 @@ SIGNATURES = {
                                           c_void_p, c_size_t, c_void_p, c_int64, c_void_p]),
     "aa_adam_step": (c_int, [POINTER(AdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double,
                              c_double, c_void_p]),
+    "aa_clip_grad_norm_workspace_bytes": (c_size_t, [POINTER(GradTensor), c_int32]),
+    "aa_clip_grad_norm": (c_int, [POINTER(GradTensor), c_int32, c_float, c_void_p, c_void_p, c_size_t, c_void_p]),
     "aa_synth_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_int64, c_double, c_double, c_void_p]),
     "aa_read_probe": (c_int, [c_void_p, c_size_t, c_void_p, c_int32, c_void_p]),
 }

@@ -306,6 +306,99 @@ __global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* x, int64_t l
   for (; j < V; j += CE_THREADS) dr[j] = (expf(xr[j] - L) - (j == t ? 1.f : 0.f)) * scale;
 }
 
+// ---- clip_grad_norm_ (torch.nn.utils.clip_grad_norm_(params, max_norm), 2-norm; train.py:210) --------
+// torch: norms = _foreach_norm(grads); total = vector_norm(stack(norms)); coef = max_norm / (total +
+// 1e-6); grads *= clamp(coef, max=1).  Here: k_clip_sumsq writes one fp32 sum of squares per workgroup
+// (CLIP_CHUNK elements of one tensor, a fixed order), k_clip_norm adds each tensor's partials in block
+// order, takes the norm, combines the tensors' norms as torch does and writes (total, coef); k_clip_scale
+// multiplies every gradient by the clamped coefficient (a multiply by exactly 1.0 when no clip is due,
+// as torch's).  Three launches, one host call.
+constexpr int CLIP_THREADS = 256, CLIP_VEC = 4, CLIP_ROUNDS = 8;
+constexpr int CLIP_CHUNK = CLIP_THREADS * CLIP_VEC * CLIP_ROUNDS;  // 8192 elements per workgroup
+struct ClipArgs {
+  int n;
+  int aligned;                            // bit i: tensor i is 16-byte aligned
+  int64_t blk0[AA_CLIP_MAX_TENSORS + 1];  // first workgroup of tensor i (prefix sum)
+  int64_t numel[AA_CLIP_MAX_TENSORS];
+  float* g[AA_CLIP_MAX_TENSORS];
+  float* part;      // [workgroups] sums of squares
+  float* out;       // [2]: total norm, clamped coefficient
+  float max_norm;
+};
+__device__ __forceinline__ int clip_tensor(const ClipArgs& a, int64_t blk) {
+  int t = 0;
+  while (t + 1 < a.n && blk >= a.blk0[t + 1]) ++t;
+  return t;
+}
+__global__ __launch_bounds__(CLIP_THREADS) void k_clip_sumsq(ClipArgs a) {
+  const int64_t blk = blockIdx.x;
+  const int t = clip_tensor(a, blk);
+  const int64_t base = (blk - a.blk0[t]) * CLIP_CHUNK, n = a.numel[t];
+  const float* __restrict__ G = a.g[t];
+  float acc = 0.f;
+  if (((a.aligned >> t) & 1) && base + CLIP_CHUNK <= n) {
+    float4 g4[CLIP_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < CLIP_ROUNDS; ++r)
+      g4[r] = *reinterpret_cast<const float4*>(G + base + ((int64_t)r * CLIP_THREADS + threadIdx.x) * CLIP_VEC);
+#pragma unroll
+    for (int r = 0; r < CLIP_ROUNDS; ++r) {
+      acc = fmaf(g4[r].x, g4[r].x, acc);
+      acc = fmaf(g4[r].y, g4[r].y, acc);
+      acc = fmaf(g4[r].z, g4[r].z, acc);
+      acc = fmaf(g4[r].w, g4[r].w, acc);
+    }
+  } else {
+    const int64_t end = base + CLIP_CHUNK < n ? base + CLIP_CHUNK : n;
+    for (int64_t i = base + threadIdx.x; i < end; i += CLIP_THREADS) acc = fmaf(G[i], G[i], acc);
+  }
+  __shared__ float red[CLIP_THREADS / 64];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) a.part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(CLIP_THREADS) void k_clip_norm(ClipArgs a) {
+  __shared__ float red[CLIP_THREADS / 64];
+  __shared__ float norms[AA_CLIP_MAX_TENSORS];
+  for (int t = 0; t < a.n; ++t) {
+    float acc = 0.f;
+    for (int64_t i = a.blk0[t] + threadIdx.x; i < a.blk0[t + 1]; i += CLIP_THREADS) acc += a.part[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) norms[t] = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int t = 0; t < a.n; ++t) s = fmaf(norms[t], norms[t], s);
+    const float total = sqrtf(s);
+    const float coef = a.max_norm / (total + 1e-6f);
+    a.out[0] = total;
+    a.out[1] = coef > 1.f ? 1.f : coef;  // clamp(max = 1) that keeps a NaN, as torch.clamp does
+  }
+}
+__global__ __launch_bounds__(CLIP_THREADS) void k_clip_scale(ClipArgs a) {
+  const int64_t blk = blockIdx.x;
+  const int t = clip_tensor(a, blk);
+  const int64_t base = (blk - a.blk0[t]) * CLIP_CHUNK, n = a.numel[t];
+  float* __restrict__ G = a.g[t];
+  const float c = a.out[1];
+  if (((a.aligned >> t) & 1) && base + CLIP_CHUNK <= n) {
+#pragma unroll
+    for (int r = 0; r < CLIP_ROUNDS; ++r) {
+      float4* q = reinterpret_cast<float4*>(G + base + ((int64_t)r * CLIP_THREADS + threadIdx.x) * CLIP_VEC);
+      float4 v = *q;
+      v.x *= c; v.y *= c; v.z *= c; v.w *= c;
+      *q = v;
+    }
+  } else {
+    const int64_t end = base + CLIP_CHUNK < n ? base + CLIP_CHUNK : n;
+    for (int64_t i = base + threadIdx.x; i < end; i += CLIP_THREADS) G[i] *= c;
+  }
+}
+
 }  // namespace aa_optim
 
 using namespace aa_optim;
@@ -355,6 +448,57 @@ int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double l
     if (e != hipSuccess) return (int)e;
   }
   return AA_OK;
+}
+
+static bool clip_args(const aa_grad_tensor* t, int32_t n, ClipArgs* a, int64_t* blocks) {
+  a->n = 0;
+  a->aligned = 0;
+  *blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (t[i].numel < 0) return false;
+    if (t[i].numel == 0) continue;
+    const int k = a->n++;
+    a->g[k] = t[i].grad;
+    a->numel[k] = t[i].numel;
+    if (((uintptr_t)t[i].grad & 15) == 0) a->aligned |= 1 << k;
+    a->blk0[k] = *blocks;
+    *blocks += (t[i].numel + CLIP_CHUNK - 1) / CLIP_CHUNK;
+  }
+  a->blk0[a->n] = *blocks;
+  return true;
+}
+
+size_t aa_clip_grad_norm_workspace_bytes(const aa_grad_tensor* tensors, int32_t n) {
+  if (n < 0 || n > AA_CLIP_MAX_TENSORS || (n > 0 && !tensors)) return 0;
+  ClipArgs a;
+  int64_t blocks;
+  if (!clip_args(tensors, n, &a, &blocks)) return 0;
+  return (size_t)(blocks + 2) * sizeof(float);
+}
+
+int aa_clip_grad_norm(const aa_grad_tensor* tensors, int32_t n, float max_norm, float* total_norm, void* workspace,
+                      size_t workspace_bytes, aa_stream_t stream) {
+  if (n < 0 || n > AA_CLIP_MAX_TENSORS) return AA_ERR_SHAPE;
+  if ((n > 0 && !tensors) || !total_norm || !workspace) return AA_ERR_NULL;
+  ClipArgs a;
+  int64_t blocks;
+  if (!clip_args(tensors, n, &a, &blocks)) return AA_ERR_SHAPE;
+  for (int k = 0; k < a.n; ++k)
+    if (!a.g[k]) return AA_ERR_NULL;
+  if (workspace_bytes < (size_t)(blocks + 2) * sizeof(float)) return AA_ERR_BUFFER;
+  if (blocks > 0x7fffffff) return AA_ERR_SHAPE;
+  float* ws = (float*)workspace;
+  a.out = ws;
+  a.part = ws + 2;
+  a.max_norm = max_norm;
+  hipStream_t st = (hipStream_t)stream;
+  if (blocks > 0) hipLaunchKernelGGL(k_clip_sumsq, dim3((unsigned)blocks), dim3(CLIP_THREADS), 0, st, a);
+  hipLaunchKernelGGL(k_clip_norm, dim3(1), dim3(CLIP_THREADS), 0, st, a);
+  if (blocks > 0) hipLaunchKernelGGL(k_clip_scale, dim3((unsigned)blocks), dim3(CLIP_THREADS), 0, st, a);
+  // the total norm, as torch returns it (a device scalar)
+  const hipError_t e = hipMemcpyAsync(total_norm, ws, sizeof(float), hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipGetLastError();
 }
 
 size_t aa_cross_entropy_workspace_bytes(int32_t N) {

@@ -60,34 +60,30 @@ class Adam(torch.optim.Optimizer):
             live = [p for p in group["params"] if p.grad is not None]
             if not live:
                 continue
-            # the validated launch table of this group, reused while the parameters, their gradient
-            # tensors and the state tensors (load_state_dict replaces them) are the ones it was built
-            # from (the caching allocator hands back the same gradient blocks step after step): the
-            # per-tensor checks and the table build then cost nothing per step
-            state = self.state
             # the plan (validated parameters, their state, the launch tables) is reused while the
-            # parameters and their state tensors are the same objects (load_state_dict replaces the
-            # state: rebuilt); the gradients are new tensors every step (zero_grad sets them to None,
-            # and the caching allocator need not hand back the same blocks), so they are checked and
-            # their pointers written into the tables on every step
-            ident = tuple((id(p), *(id(x) for x in state[p].values())) if p in state else (id(p),) for p in live)
+            # group's live parameters and the state dict are the same objects (load_state_dict replaces
+            # the state dict: rebuilt); the gradients are new tensors every step (zero_grad sets them to
+            # None and the caching allocator need not hand back the same blocks), so they are checked
+            # and their pointers written into the tables on every step
+            ident = (id(self.state), tuple(map(id, live)))
             plan = self._tables.get(gi)
             if plan is None or plan[0] != ident:
                 plan = self._plan(live, ident)
                 if len(self._tables) > 16:
                     self._tables.clear()
                 self._tables[gi] = plan
-            for p, (arr, i) in zip(live, plan[3]):
+            _, sbuf, calls, gslots = plan
+            for p, (arr, i) in zip(live, gslots):
                 g = p.grad
                 if g.dtype is not torch.float32 or g.is_sparse or not g.is_cuda or not g.is_contiguous() \
                         or g.shape != p.shape or g.device != p.device:
                     self._check_grad(p)
                 arr[i].grad = g.data_ptr()
-            _, steps, calls, _ = plan
-            # the step counts, as torch.optim.Adam keeps them (CPU float32 tensors), one foreach add
-            torch._foreach_add_(steps, 1.0)
+            # the step counts, kept as torch.optim.Adam keeps them (a CPU float32 tensor per parameter),
+            # are 0-d views of one buffer: one add per step (a foreach add over 21 CPU scalars cost ~70 us)
+            sbuf.add_(1.0)
             for dev, first, arr, n in calls:
-                step = float(steps[first].item())
+                step = float(sbuf[first].item())
                 with torch.cuda.device(dev):
                     rc = lib.aa_adam_step(arr, n, step, group["lr"], beta1, beta2, group["eps"],
                                           group["weight_decay"], _lib.stream_handle())
@@ -97,18 +93,23 @@ class Adam(torch.optim.Optimizer):
     def _plan(self, live, ident):
         """Validate the group's live parameters (a rejected tensor leaves no parameter with a step
         count for an update that never ran: torch's bias correction would drift), create missing
-        state, and group the tensors that share a device and a step count into launch tables."""
+        state, move the step counts into one buffer (each parameter's state keeps its own 0-d CPU
+        float32 ``step`` tensor, a view), and group the tensors that share a device and a step count
+        into launch tables."""
         for p in live:
             self._check_grad(p)
-        steps, by_step = [], {}
+        sbuf = torch.zeros(len(live), dtype=torch.float32)
+        by_step = {}
         for i, p in enumerate(live):
             st = self.state[p]
             if len(st) == 0:
                 st["step"] = torch.tensor(0.0, dtype=torch.float32)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            steps.append(st["step"])
-            by_step.setdefault((p.device, float(st["step"].item())), []).append(
+            v = float(st["step"].item())
+            sbuf[i] = v
+            st["step"] = sbuf[i]
+            by_step.setdefault((p.device, v), []).append(
                 (i, (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                      p.numel())))
         calls, gslots = [], [None] * len(live)
@@ -117,7 +118,7 @@ class Adam(torch.optim.Optimizer):
             calls.append((dev, rows[0][0], arr, len(rows)))
             for j, (i, _) in enumerate(rows):
                 gslots[i] = (arr, j)
-        return ident, steps, calls, gslots
+        return ident, sbuf, calls, gslots
 
     @staticmethod
     def _check_grad(p):
@@ -129,6 +130,59 @@ class Adam(torch.optim.Optimizer):
             raise RuntimeError("adaptive_amd.optim.Adam: parameters and gradients must be contiguous")
         if p.grad.shape != p.shape or p.grad.device != p.device:
             raise RuntimeError("adaptive_amd.optim.Adam: a gradient's shape/device differs from its parameter's")
+
+
+_clip_cache = {}
+
+
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_if_nonfinite: bool = False,
+                    foreach=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ with the 2-norm (train.py:210: ``clip_grad_norm_(lstm params,
+    cf.clip)``) for fp32 contiguous GPU gradients, as one ``aa_clip_grad_norm`` host call (three
+    launches per 24 tensors): per-tensor norms, the total over them, every gradient scaled in place by
+    ``min(max_norm / (total + 1e-6), 1)``.  Returns the total norm as a 0-d device tensor, as torch
+    does.  Other norm types raise ``NotImplementedError``; CPU tensors raise ``RuntimeError``."""
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if float(norm_type) != 2.0:
+        raise NotImplementedError("adaptive_amd.optim.clip_grad_norm_: only the 2-norm (train.py:210)")
+    if not grads:
+        return torch.tensor(0.0)
+    dev = grads[0].device
+    for g in grads:
+        if g.dtype is not torch.float32 or g.is_sparse or not g.is_cuda or not g.is_contiguous() or g.device != dev:
+            _require_hip(g, "gradient")
+            if g.is_sparse or not g.is_contiguous() or g.device != dev:
+                raise RuntimeError("adaptive_amd.optim.clip_grad_norm_: gradients must be dense, contiguous and "
+                                   "on one device")
+    lib = _lib.load()
+    if len(grads) > _lib.CLIP_MAX_TENSORS:
+        raise ValueError(f"adaptive_amd.optim.clip_grad_norm_: at most {_lib.CLIP_MAX_TENSORS} tensors")
+    key = (dev, tuple(g.numel() for g in grads))
+    ent = _clip_cache.get(key)
+    if ent is None:
+        arr = (_lib.GradTensor * len(grads))(*[_lib.GradTensor(None, g.numel()) for g in grads])
+        nbytes = lib.aa_clip_grad_norm_workspace_bytes(arr, len(grads))
+        if nbytes == 0:
+            raise RuntimeError("adaptive_amd.optim.clip_grad_norm_: invalid gradient table")
+        ent = (arr, torch.empty(nbytes, dtype=torch.uint8, device=dev))
+        if len(_clip_cache) > 16:
+            _clip_cache.clear()
+        _clip_cache[key] = ent
+    arr, ws = ent
+    for i, g in enumerate(grads):
+        arr[i].grad = g.data_ptr()
+    total = torch.empty((), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.aa_clip_grad_norm(arr, len(grads), float(max_norm), total.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   _lib.stream_handle())
+    _lib.check(rc, "clip_grad_norm")
+    if error_if_nonfinite and not bool(torch.isfinite(total)):
+        raise RuntimeError(f"The total norm of order {float(norm_type)} for gradients from `parameters` is "
+                           "non-finite, so it cannot be clipped.")
+    return total
+
 
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
@@ -193,4 +247,4 @@ class CrossEntropyLoss(torch.nn.Module):
         return cross_entropy(input, target, self.ignore_index)
 
 
-__all__ = ["Adam", "CrossEntropyLoss", "cross_entropy"]
+__all__ = ["Adam", "CrossEntropyLoss", "clip_grad_norm_", "cross_entropy"]

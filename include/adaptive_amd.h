@@ -371,6 +371,20 @@ typedef struct aa_adam_tensor {
 AA_API int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double lr, double beta1,
                         double beta2, double eps, double weight_decay, aa_stream_t stream);
 
+/* aa_clip_grad_norm: torch.nn.utils.clip_grad_norm_(params, max_norm) with the 2-norm (train.py:210
+ * clips the LSTM's gradients to 5): total = sqrt(sum_i ||g_i||^2) over the tensors' norms, coef =
+ * max_norm / (total + 1e-6), every gradient multiplied in place by min(coef, 1) (NaN kept); the total
+ * norm is written to total_norm (a device float).  Fixed reduction order: deterministic.  Up to
+ * AA_CLIP_MAX_TENSORS tensors; workspace from aa_clip_grad_norm_workspace_bytes (0 = invalid input). */
+#define AA_CLIP_MAX_TENSORS 24
+typedef struct aa_grad_tensor {
+  float* grad;
+  int64_t numel;
+} aa_grad_tensor;
+AA_API size_t aa_clip_grad_norm_workspace_bytes(const aa_grad_tensor* tensors, int32_t n);
+AA_API int aa_clip_grad_norm(const aa_grad_tensor* tensors, int32_t n, float max_norm, float* total_norm,
+                             void* workspace, size_t workspace_bytes, aa_stream_t stream);
+
 /* Measurement helper (bench.py's roofline block; not on the decode path): one streaming read of
  * nbytes (multiple of 16, 16-B aligned) from src by `blocks` workgroups, each writing its partial sum
  * to out[block].  Timed over a buffer resident in the 256 MiB Infinity Cache it gives the MALL-served

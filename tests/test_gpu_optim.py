@@ -162,13 +162,13 @@ def test_adam_reused_plan_and_state_reload(gpu_device):
 
 def test_train_closure_with_hip_loss_and_adam(gpu_device):
     """train.py:197-219 closure, three steps at B=16, T=10 (fp32 GEMMs, so that ulp-level
-    differences are not amplified by bf16 operand rounding): HIP CrossEntropyLoss + HIP Adam against
+    differences are not amplified by bf16 operand rounding): HIP CrossEntropyLoss + clip_grad_norm_ + Adam against
     torch's on a second copy of the same model: the losses and parameters agree to fp32 rounding (the
     forward/backward kernels are the same, so only the loss and the update differ)."""
     from torch.nn.utils.rnn import pack_padded_sequence
     from adaptive_amd import Config, Encoder2Decoder
     from adaptive_amd.adaptive_attention import synthetic_features
-    from adaptive_amd.optim import Adam, CrossEntropyLoss
+    from adaptive_amd.optim import Adam, CrossEntropyLoss, clip_grad_norm_
     B, T = 16, 10
     rng = np.random.default_rng(0)
     lengths = sorted(rng.integers(T // 2, T + 1, size=B).tolist(), reverse=True)
@@ -183,13 +183,14 @@ def test_train_closure_with_hip_loss_and_adam(gpu_device):
         model.train_bf16 = False
         opt = (Adam if hip else torch.optim.Adam)(model.parameters(), lr=1e-3)
         crit = CrossEntropyLoss() if hip else torch.nn.CrossEntropyLoss()
+        clip = clip_grad_norm_ if hip else torch.nn.utils.clip_grad_norm_
         losses = []
         for _ in range(3):
             model.zero_grad()
             opt.zero_grad()
             loss = crit(model(feats, caps, lengths)[0], targets)
             loss.backward()
-            torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+            clip(model.decoder.LSTM.parameters(), 5.0)
             opt.step()
             losses.append(loss.item())
         runs.append((losses, {k: v.detach().clone() for k, v in model.state_dict().items()}))
@@ -198,3 +199,42 @@ def test_train_closure_with_hip_loss_and_adam(gpu_device):
     for k in sr:
         err = (sa[k] - sr[k]).abs().max().item()
         assert err <= 2e-5 * max(1.0, sr[k].abs().max().item()), (k, err)
+
+
+@pytest.mark.parametrize("max_norm", [5.0, 1e30, 0.0])
+def test_clip_grad_norm_matches_torch(gpu_device, max_norm):
+    """clip_grad_norm_ (train.py:210) vs torch.nn.utils.clip_grad_norm_: tensor sizes either side of
+    the kernel's 8192-element chunk, an empty tensor, an unaligned view, a parameter without a
+    gradient; the total norm to fp32 rounding (the sum order differs), the clipped gradients to a few
+    ulps (the same multiply by a coefficient that differs by at most that), and no clip due leaves the
+    gradients bit-identical (torch multiplies by exactly 1.0 then too).  New gradient tensors on the
+    second call (the cached table takes their pointers)."""
+    from adaptive_amd.optim import clip_grad_norm_
+    buf = torch.empty(20001, device=gpu_device)
+    shapes = [(4096, 1024), (4096,), (8192,), (8193,), (8191,), (1,), (0,), (3, 7)]
+    for rep in range(2):
+        torch.manual_seed(rep)
+        pa = [torch.zeros(s, device=gpu_device, requires_grad=True) for s in shapes]
+        pa.append(buf[1:].detach().requires_grad_())  # 4 bytes into its buffer: the scalar path
+        pa.append(torch.zeros(5, device=gpu_device, requires_grad=True))  # no gradient
+        for i, p in enumerate(pa[:-1]):
+            p.grad = torch.randn(p.shape, device=gpu_device) * 10.0 ** -(i % 3)
+        # the unaligned parameter's gradient is an unaligned view too (a fresh one on each call)
+        pa[-2].grad = torch.empty(20001, device=gpu_device)[1:].copy_(pa[-2].grad)
+        assert pa[-2].grad.data_ptr() % 16 != 0
+        pr = [p.detach().clone().requires_grad_() for p in pa]
+        for a, r in zip(pa, pr):
+            r.grad = None if a.grad is None else a.grad.clone()
+        ga0 = [None if p.grad is None else p.grad.clone() for p in pa]
+        ta = clip_grad_norm_(pa, max_norm)
+        tr = torch.nn.utils.clip_grad_norm_(pr, max_norm)
+        assert ta.shape == () and ta.is_cuda and ta.dtype == torch.float32
+        torch.testing.assert_close(ta, tr, rtol=1e-5, atol=0)
+        for a, r, g0 in zip(pa, pr, ga0):
+            if a.grad is None:
+                assert r.grad is None
+                continue
+            if max_norm >= 1e30:
+                assert torch.equal(a.grad, g0)
+            else:
+                torch.testing.assert_close(a.grad, r.grad, rtol=2e-5, atol=0)

@@ -18,7 +18,7 @@ from adaptive_amd import optim as aa_optim  # noqa: E402
 from adaptive_amd.adaptive_attention import synthetic_features  # noqa: E402
 
 NAMES = ("aa_train_forward_aux", "aa_train_backward_aux", "aa_cross_entropy_forward", "aa_cross_entropy_backward",
-         "aa_adam_step", "aa_train_workspace_bytes")
+         "aa_adam_step", "aa_clip_grad_norm", "aa_train_workspace_bytes")
 
 
 class Timed:
@@ -48,14 +48,14 @@ def main():
     opt = aa_optim.Adam(model.parameters(), lr=1e-4)
     crit = aa_optim.CrossEntropyLoss()
     for _ in range(10):
-        step(model, opt, crit, feats, caps, lengths)
+        step(model, opt, crit, feats, caps, lengths, aa_optim.clip_grad_norm_)
     torch.cuda.synchronize()
     for t in timers.values():
         t.t, t.n = 0.0, 0
     n = 40
     t0 = time.perf_counter()
     for _ in range(n):
-        step(model, opt, crit, feats, caps, lengths)
+        step(model, opt, crit, feats, caps, lengths, aa_optim.clip_grad_norm_)
     host = (time.perf_counter() - t0) / n
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / n

@@ -47,7 +47,7 @@ def main():
         e = time.perf_counter()
         loss.backward()
         f = time.perf_counter()
-        torch.nn.utils.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
+        aa_optim.clip_grad_norm_(model.decoder.LSTM.parameters(), 5.0)
         g = time.perf_counter()
         opt.step()
         h = time.perf_counter()
