@@ -325,6 +325,155 @@ static void reduce_launch(const TG& g, hipStream_t s) {
     hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)(((int64_t)g.M * g.N + 255) / 256)), dim3(256), 0, s, g);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_tgemm on 128 x 128 tiles for a bf16 step (AA_TRAIN_BF16): the same operand layouts (A
+// row-major or transposed, W in layouts 0 / 1), RNE rounding while staging, bias / act / row maps /
+// accumulate and split-K partials as k_tgemm; a workgroup computes a 128 x 128 tile (four waves of
+// 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16 blocks, k_bgemm's MFMA arrangement), 64-deep K steps
+// double-buffered in LDS.  Twice k_tgemm's FLOP per staged byte and four MFMAs per fragment pair read.
+// LDS rows of 72 bf16 (144 B) with the 16-B chunk index XOR-swizzled by (row / 8) % 8: the
+// transposed operands are staged as 2-byte stores down a column of rows 8 apart, which without the
+// swizzle fall into two banks (8-way conflicts); with it into 16.  The 16-B fragment reads stay
+// conflict-free (8 consecutive rows share the swizzle).
+// ---------------------------------------------------------------------------------------------
+constexpr int T8_T = 128, T8_KS = 64, T8_LD = T8_KS + 8;
+__device__ __forceinline__ int t8_off(int r, int k) {  // bf16 index of (row r, k) in a swizzled tile
+  return r * T8_LD + ((((k >> 3) ^ (r >> 3)) & 7) << 3) + (k & 7);
+}
+__global__ __launch_bounds__(256, 2) void k_tgemm128(TG g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][T8_T * T8_LD];
+  const int tilesN = (g.N + T8_T - 1) / T8_T;
+  const int split = blockIdx.x % g.splits, tile = blockIdx.x / g.splits;
+  const int mt = tile / tilesN, nt = tile % tilesN;
+  const int kbeg = split * g.kper, kend = g.splits > 1 ? (kbeg + g.kper < g.K ? kbeg + g.kper : g.K) : g.K;
+  const int m0 = mt * T8_T, n0 = nt * T8_T;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool a4 = ((g.lda & 3) == 0) && ((((uintptr_t)g.A) & 15) == 0);
+  const bool w4 = ((g.ldw & 3) == 0) && ((((uintptr_t)g.W) & 15) == 0);
+  float ra[4][8], rw[4][8];
+  auto load8 = [&](float (&r)[8], const float* base) {
+    const float4 x = *reinterpret_cast<const float4*>(base), y = *reinterpret_cast<const float4*>(base + 4);
+    r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w; r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+  };
+  // piece i of this thread: K-contiguous operands (A with at = 0, W with wm = 0) -> row q >> 3,
+  // k 8 (q & 7) (8 lanes per 256-B row segment); transposed ones -> k q >> 4, rows 8 (q & 15) .. + 7
+  // (16 lanes per 512-B segment of a k row); q = t + 256 i
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + 256 * i;
+      if (!g.at) {
+        const int r = q >> 3, kq = (q & 7) * 8, m = m0 + r, k = k0 + kq;
+        const int64_t base = (int64_t)(m < g.M ? (g.arow ? g.arow[m] : m) : 0) * g.lda;
+        if (a4 && m < g.M && k + 8 <= kend) load8(ra[i], g.A + base + k);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ra[i][e] = (m < g.M && k + e < kend) ? g.A[base + k + e] : 0.f;
+      } else {
+        const int k = k0 + (q >> 4), mq = m0 + (q & 15) * 8;
+        if (a4 && k < kend && mq + 8 <= g.M) load8(ra[i], g.A + (int64_t)k * g.lda + mq);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ra[i][e] = (k < kend && mq + e < g.M) ? g.A[(int64_t)k * g.lda + mq + e] : 0.f;
+      }
+      if (g.wm == 0) {
+        const int r = q >> 3, kq = (q & 7) * 8, n = n0 + r, k = k0 + kq;
+        const int64_t base = (int64_t)(n < g.N ? n : 0) * g.ldw;
+        if (w4 && n < g.N && k + 8 <= kend) load8(rw[i], g.W + base + k);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rw[i][e] = (n < g.N && k + e < kend) ? g.W[base + k + e] : 0.f;
+      } else {
+        const int k = k0 + (q >> 4), nq = n0 + (q & 15) * 8;
+        if (w4 && k < kend && nq + 8 <= g.N) load8(rw[i], g.W + (int64_t)k * g.ldw + nq);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rw[i][e] = (k < kend && nq + e < g.N) ? g.W[(int64_t)k * g.ldw + nq + e] : 0.f;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    __bf16* As = lds[buf][0];
+    __bf16* Ws = lds[buf][1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + 256 * i;
+      if (!g.at) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)ra[i][e];
+        *reinterpret_cast<bf16x8*>(As + t8_off(q >> 3, (q & 7) * 8)) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) As[t8_off((q & 15) * 8 + e, q >> 4)] = (__bf16)ra[i][e];
+      }
+      if (g.wm == 0) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)rw[i][e];
+        *reinterpret_cast<bf16x8*>(Ws + t8_off(q >> 3, (q & 7) * 8)) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Ws[t8_off((q & 15) * 8 + e, q >> 4)] = (__bf16)rw[i][e];
+      }
+    }
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
+  const int nk = (kend - kbeg + T8_KS - 1) / T8_KS;
+  gload(kbeg);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * T8_KS);
+    const __bf16* As = lds[buf][0];
+    const __bf16* Ws = lds[buf][1];
+#pragma unroll
+    for (int kb = 0; kb < T8_KS / 16; ++kb) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const bf16x8*>(As + t8_off(wm * 64 + x * 32 + li, 16 * kb + 8 * lh));
+#pragma unroll
+      for (int y = 0; y < 2; ++y) b[y] = *reinterpret_cast<const bf16x8*>(Ws + t8_off(wn * 64 + y * 32 + li, 16 * kb + 8 * lh));
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x], b[y], acc[x][y], 0, 0, 0);
+    }
+    if (ks + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int y = 0; y < 2; ++y) {
+    const int col = n0 + wn * 64 + y * 32 + li;
+    if (col >= g.N) continue;
+    const float bv = (g.bias ? g.bias[col] : 0.f) + (g.bias2 ? g.bias2[col] : 0.f);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + x * 32 + acc_row(r, lane);
+        if (m >= g.M) continue;
+        if (g.splits > 1) {
+          g.part[(int64_t)split * g.M * g.N + (int64_t)m * g.N + col] = acc[x][y][r];
+        } else {
+          float v = acc[x][y][r] + bv;
+          if (g.act == 1) v = reluf_(v);
+          else if (g.act == 2) v = tanhf(v);
+          float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
+          *dst = g.accumulate ? *dst + v : v;
+        }
+      }
+  }
+}
+
 // k_tgemm's split-K bound (floats of partials): its split counts, and so its fp32 sums, as before
 // the scratch grew for k_bgemm
 constexpr size_t TG_SPLIT_CAP = (size_t)4 << 20;
@@ -348,9 +497,45 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
                  const float* bias2 = nullptr, int act = 0, const int* arow = nullptr, const int* crow = nullptr,
                  bool defer = false) {
   if (M <= 0 || N <= 0) return 0;
+  const hipStream_t s = gc.s;
+  static const bool tlog = [] {  // AA_TG_LOG=1: one stderr line per GEMM (shape attribution of a trace)
+    const char* e = getenv("AA_TG_LOG");
+    return e && atoi(e) == 1;
+  }();
+  if (tlog) fprintf(stderr, "tgemm M %d N %d K %d at %d wm %d acc %d stream %p\n", M, N, K, at, wm, accumulate, (void*)s);
+  // AA_TG128=1, bf16 weight gradients (both operands transposed, K >= 1024: dW_hh, dW_ih, dW_x, dW_h
+  // over all T B rows): 128 x 128 tiles (k_tgemm128), split along K to ~512 workgroups (>= 256 deep
+  // each) -- 30.7 / 31.0 us against 41.7 / 76.1 us for dW_hh / dW_ih on the 64 x 64 engine (split to
+  // 1024 workgroups, four times the partials), but they run on the aux stream beside the LSTM
+  // backward and the whole step did not gain (750 vs 752 steps/s); for the GEMMs reading one operand
+  // along K the 64 x 64 engine measured faster (profiles/r06v_train_gemm_engines.txt)
+  static const bool t128 = [] {  // AA_TG128=1: the deep weight gradients on k_tgemm128 (off: no gain in the step)
+    const char* e = getenv("AA_TG128");
+    return e && atoi(e) == 1;
+  }();
+  if (t128 && gc.bf16 && at == 1 && wm == 1 && M >= 128 && N >= 128 && (int64_t)M * N >= 128 * 256 && K >= 1024) {
+    const int tiles8 = ((M + T8_T - 1) / T8_T) * ((N + T8_T - 1) / T8_T);
+    int sp = 1;
+    if (tiles8 < 256 && K >= 512 && gc.split) {
+      sp = (512 + tiles8 - 1) / tiles8;
+      if (sp > K / 256) sp = K / 256;
+      const size_t capsp = gc.cap / ((size_t)M * N);
+      if ((size_t)sp > capsp) sp = (int)capsp;
+      if (sp < 2) sp = 1;
+    }
+    int kp = K;
+    if (sp > 1) {
+      kp = ((K + sp - 1) / sp + T8_KS - 1) / T8_KS * T8_KS;
+      sp = (K + kp - 1) / kp;
+    }
+    TG g{M, N, K, A, lda, arow, at, W, ldw, wm, C, ldc, crow, bias, bias2, accumulate, act, sp, kp,
+         sp > 1 ? gc.split : nullptr};
+    hipLaunchKernelGGL(k_tgemm128, dim3(tiles8 * sp), dim3(256), 0, s, g);
+    if (sp > 1 && !defer) reduce_launch(g, s);
+    return sp;
+  }
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
   int splits = 1;
-  const hipStream_t s = gc.s;
   // few tiles: split to ~256 workgroups (>= 128 deep each); long K over < 512 tiles (the vocab-sized
   // backward GEMMs, the weight gradients over all T*B rows): split to ~1024 (>= 512 deep each)
   const bool small = tiles < 128 && K >= 256, deep = tiles < 512 && K >= 1024;
@@ -1496,6 +1681,39 @@ __global__ __launch_bounds__(256) void k_rowsum_pp(const float* __restrict__ X, 
 // ---------------------------------------------------------------------------------------------
 constexpr size_t TR_SPLIT_FLOATS = (size_t)16 << 20;  // 64 MB split-K scratch (k_bgemm's splits of dU / dW_a)
 
+// Transposed copies of weights, several matrices per launch: dst_i[c][r] = src_i[r][c] (src row-major
+// [rows][cols], dst [cols][ld], zero for rows <= r < ld), 64 x 64 tiles through LDS (reads along c, writes
+// along r, both coalesced).  Exact copies: a GEMM reading the copy along K multiplies the same values in
+// the same order as one reading the original down its columns.
+constexpr int WT_MAX = 8;
+constexpr int WT_LDP = (aa::P + 3) / 4 * 4;  // the [H][P] copies: rows padded to whole 16-B groups
+struct WTArgs {
+  int n;
+  const float* src[WT_MAX];
+  float* dst[WT_MAX];
+  int rows[WT_MAX], cols[WT_MAX], ld[WT_MAX];
+  int blk0[WT_MAX + 1];  // first tile of matrix i
+};
+__global__ __launch_bounds__(256) void k_wT(WTArgs a) {
+  __shared__ float tile[64][65];
+  int i = 0;
+  while (i + 1 < a.n && (int)blockIdx.x >= a.blk0[i + 1]) ++i;
+  const int tb = blockIdx.x - a.blk0[i], rows = a.rows[i], cols = a.cols[i], ld = a.ld[i];
+  const int tr = (ld + 63) / 64;
+  const int r0 = (tb % tr) * 64, c0 = (tb / tr) * 64, t = threadIdx.x;
+  const float* __restrict__ src = a.src[i];
+  float* __restrict__ dst = a.dst[i];
+  for (int j = t; j < 64 * 64; j += 256) {
+    const int rr = j / 64, cc = j % 64, r = r0 + rr, c = c0 + cc;
+    tile[rr][cc] = (r < rows && c < cols) ? src[(int64_t)r * cols + c] : 0.f;
+  }
+  __syncthreads();
+  for (int j = t; j < 64 * 64; j += 256) {
+    const int cc = j / 64, rr = j % 64, c = c0 + cc, r = r0 + rr;
+    if (c < cols && r < ld) dst[(int64_t)c * ld + r] = tile[rr][cc];
+  }
+}
+
 struct TrainWS {
   float *a_g, *V, *vg, *h0, *c0, *VWv, *X, *PRE, *G4, *GA, *Hs, *Cs, *SG, *S, *PG, *PS, *alpha, *beta, *ctx, *U;
   int* prow;
@@ -1511,6 +1729,9 @@ struct TrainWS {
   bf16x8 *whf, *whb;
   __bf16 *hb[2], *dgb[2];
   int *trank, *tcount, *torder, *tsmall;
+  // the weights the backward multiplies by untransposed (dx = dG W), stored transposed [in][out] by
+  // the forward (k_wT, on aux): the backward's GEMMs then read both operands along K
+  float *wgT, *wsT, *wvT, *wxT, *whT, *whhT, *wihT;
 };
 
 // step groups of the attention backward's per-image sums over t (k_tr_atb_img; they were the
@@ -1596,6 +1817,13 @@ static TrainWS carve_train(char* base, const aa_dims& d, int B, int T, int Nmax,
       w.dgb[i] = c.take<__bf16>((size_t)B * 4 * H);
     }
   }
+  w.wgT = c.take<float>(H * WT_LDP);
+  w.wsT = c.take<float>(H * WT_LDP);
+  w.wvT = c.take<float>(H * WT_LDP);
+  w.wxT = c.take<float>(2 * E * H);
+  w.whT = c.take<float>(H * H);
+  w.whhT = c.take<float>(H * 4 * H);
+  w.wihT = c.take<float>(2 * E * 4 * H);
   *bytes = c.off;
   return w;
 }
@@ -1749,6 +1977,24 @@ int aa_train_forward_aux(const aa_ref_weights* w, const aa_dims* dims, const flo
   tgemm(ga, B * P, P, H, s.V, H, 0, w->att_affine_v_w, H, 0, s.VWv, PP);  // VWv = V W_v^T
   // the packed rows of the scores (pack_padded_sequence order), also off the chain
   hipLaunchKernelGGL(k_tr_prow, dim3(nblk(R)), dim3(256), 0, ga.s, lengths, B, T, s.prow);
+  // the backward's transposed weights, off the chain too (the parameters do not change until the
+  // optimizer step after the backward)
+  {
+    WTArgs a{};
+    const struct { const float* src; float* dst; int rows, cols, ld; } m[] = {
+        {w->att_affine_g_w, s.wgT, P, H, WT_LDP},   {w->att_affine_s_w, s.wsT, P, H, WT_LDP},
+        {w->att_affine_v_w, s.wvT, P, H, WT_LDP},   {w->sent_affine_x_w, s.wxT, H, 2 * E, H},
+        {w->sent_affine_h_w, s.whT, H, H, H},       {w->lstm_w_hh, s.whhT, 4 * H, H, 4 * H},
+        {w->lstm_w_ih, s.wihT, 4 * H, 2 * E, 4 * H}};
+    int tiles = 0;
+    for (const auto& x : m) {
+      a.src[a.n] = x.src; a.dst[a.n] = x.dst; a.rows[a.n] = x.rows; a.cols[a.n] = x.cols; a.ld[a.n] = x.ld;
+      a.blk0[a.n++] = tiles;
+      tiles += ((x.ld + 63) / 64) * ((x.cols + 63) / 64);
+    }
+    a.blk0[a.n] = tiles;
+    hipLaunchKernelGGL(k_wT, dim3(tiles), dim3(256), 0, ga.s, a);
+  }
   tgemm(gc, B, E, C, s.a_g, C, 0, w->enc_affine_b_w, C, 0, s.vg, E, 0, w->enc_affine_b_b, nullptr, 1);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_h0_w, C, 0, s.h0, H, 0, w->enc_affine_h0_b, nullptr, 2);
   tgemm(gc, B, H, C, s.a_g, C, 0, w->enc_affine_c0_w, C, 0, s.c0, H, 0, w->enc_affine_c0_b, nullptr, 2);
@@ -1916,11 +2162,13 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
 #undef AA_ATB
   // dH = dU (u = c_hat + h) was written by k_tr_atb_row
   f.to_aux();  // the attention's weight gradients and the V side of the encoder on aux
-  tgemm(gc, R, H, P, s.dPG, PP, 0, w->att_affine_g_w, H, 1, s.dH, H, 1);               // dh += dPG W_g
-  tgemm(gc, R, H, P, s.dPS, PP, 0, w->att_affine_s_w, H, 1, s.dS, H, 1);               // ds += dPS W_s
+  // (the weights the backward multiplies by untransposed are read from the forward's transposed
+  // copies, s.w*T: both operands along K)
+  tgemm(gc, R, H, P, s.dPG, PP, 0, s.wgT, WT_LDP, 0, s.dH, H, 1);                      // dh += dPG W_g
+  tgemm(gc, R, H, P, s.dPS, PP, 0, s.wsT, WT_LDP, 0, s.dS, H, 1);                      // ds += dPS W_s
   tgemm(ga, P, H, R, s.dPG, PP, 1, s.Hs, H, 1, GRAD(att_affine_g_w), H);                 // dW_g = dPG^T h
   tgemm(ga, P, H, R, s.dPS, PP, 1, s.S, H, 1, GRAD(att_affine_s_w), H);                  // dW_s = dPS^T s
-  tgemm(ga, B * P, H, P, s.dVWv, PP, 0, w->att_affine_v_w, H, 1, s.dV, H, 1);          // dV += dVWv W_v
+  tgemm(ga, B * P, H, P, s.dVWv, PP, 0, s.wvT, WT_LDP, 0, s.dV, H, 1);                 // dV += dVWv W_v
   tgemm(ga, P, H, B * P, s.dVWv, PP, 1, s.V, H, 1, GRAD(att_affine_v_w), H);             // dW_v = dVWv^T V
   hipLaunchKernelGGL(k_rowsum_pp, dim3(1), dim3(256), 0, sa, s.dwh, B, GRAD(att_affine_h_w));
   // encoder V = relu(A W_a^T + b) (baseline_attention.py:46-51)
@@ -1941,8 +2189,8 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
   f.to_aux();
   tgemm(ga, H, E2, R, s.dG, H, 1, s.X, E2, 1, GRAD(sent_affine_x_w), E2);               // dW_x = dG^T x
   tgemm(ga, H, H, R - B, s.dG + (size_t)B * H, H, 1, s.Hs, H, 1, GRAD(sent_affine_h_w), H);  // dW_h = dG^T h_{t-1}
-  tgemm(gc, R, E2, H, s.dG, H, 0, w->sent_affine_x_w, E2, 1, s.dX, E2);                 // dx = dG W_x
-  tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, w->sent_affine_h_w, H, 1, s.dH, H, 1);  // dh_{t-1} += dG W_h
+  tgemm(gc, R, E2, H, s.dG, H, 0, s.wxT, H, 0, s.dX, E2);                               // dx = dG W_x
+  tgemm(gc, R - B, H, H, s.dG + (size_t)B * H, H, 0, s.whT, H, 0, s.dH, H, 1);          // dh_{t-1} += dG W_h
   // LSTM backward through time (baseline_attention.py:167-178)
   AA_TRY(hipMemsetAsync(s.dh_rec, 0, (size_t)((char*)(s.dc_rec + (size_t)B * H) - (char*)s.dh_rec), st));  // adjacent
   if (gc.bf16) {
@@ -1971,7 +2219,7 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
 #undef AA_LB
     }
     f.to_aux();  // DG complete: the LSTM weight gradients on aux
-    tgemm(gc, B, H, 4 * H, s.DG, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H);
+    tgemm(gc, B, H, 4 * H, s.DG, 4 * H, 0, s.whhT, 4 * H, 0, s.dh_rec, H);
   } else {
     int S = 0;  // split count of the pending dh_rec GEMM (0: dh_rec = 0)
     for (int t = T - 1; t >= 0; --t) {
@@ -1981,7 +2229,7 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
                          S > 1 ? gc.split : s.dh_rec, S, s.dc_rec, s.GA + (size_t)t * B * 4 * H, s.Cs + o, cp, B, H,
                          s.DG + (size_t)t * B * 4 * H);
       // dh_{t-1}; the one of step 0 (into h0) is reduced into dh_rec itself
-      S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, w->lstm_w_hh, H, 1, s.dh_rec, H, 0, nullptr,
+      S = tgemm(gc, B, H, 4 * H, s.DG + (size_t)t * B * 4 * H, 4 * H, 0, s.whhT, 4 * H, 0, s.dh_rec, H, 0, nullptr,
                 nullptr, 0, nullptr, nullptr, t > 0);
     }
     f.to_aux();
@@ -1991,7 +2239,7 @@ int aa_train_backward_aux(const aa_ref_weights* w, const aa_dims* dims, const fl
   tgemm(ga, 4 * H, E2, R, s.DG, 4 * H, 1, s.X, E2, 1, GRAD(lstm_w_ih), E2);
   colsum(sa, s.DG, R, 4 * H, (int64_t)4 * H, s.csum2, GRAD(lstm_b_ih));
   AA_TRY(hipMemcpyAsync(GRAD(lstm_b_hh), GRAD(lstm_b_ih), sizeof(float) * 4 * H, hipMemcpyDeviceToDevice, sa));
-  tgemm(gc, R, E2, 4 * H, s.DG, 4 * H, 0, w->lstm_w_ih, E2, 1, s.dX, E2, 1);             // dx += dG W_ih
+  tgemm(gc, R, E2, 4 * H, s.DG, 4 * H, 0, s.wihT, 4 * H, 0, s.dX, E2, 1);               // dx += dG W_ih
   // x_t = [embed(tok); v_g] (baseline_attention.py:151-154)
   f.wait(st, tok_done);
   hipLaunchKernelGGL(k_tr_embed_bwd, dim3(R), dim3(256), 0, st, tokens, tok_ld, B, R, V, s.torder, s.trank, s.tcount,
