@@ -539,8 +539,12 @@ static int tgemm(const GemmCtx& gc, int M, int N, int K, const float* A, int64_t
   // few tiles: split to ~256 workgroups (>= 128 deep each); long K over < 512 tiles (the vocab-sized
   // backward GEMMs, the weight gradients over all T*B rows): split to ~1024 (>= 512 deep each)
   const bool small = tiles < 128 && K >= 256, deep = tiles < 512 && K >= 1024;
+  static const int deep_wg = [] {  // AA_TG_DEEP_WG: workgroups a deep split aims at (A/B probe)
+    const char* e = getenv("AA_TG_DEEP_WG");
+    return e ? atoi(e) : 1024;
+  }();
   if ((small || deep) && gc.split) {
-    splits = small ? (256 + tiles - 1) / tiles : (1024 + tiles - 1) / tiles;
+    splits = small ? (256 + tiles - 1) / tiles : (deep_wg + tiles - 1) / tiles;
     const int kmax = K / (small ? 128 : 512);
     if (splits > kmax) splits = kmax;
     const size_t capsp = (gc.cap < TG_SPLIT_CAP ? gc.cap : TG_SPLIT_CAP) / ((size_t)M * N);
@@ -809,7 +813,11 @@ static void bgemm(const GemmCtx& gc, int M, int N, int K, const __bf16* A, int64
                   int act = 0) {
   if (M <= 0 || N <= 0 || K <= 0) return;
   const int tiles = ((M + BG_T - 1) / BG_T) * ((N + BG_T - 1) / BG_T), ksteps = K / BG_KS;
-  int splits = tiles >= 512 ? 1 : (1024 + tiles - 1) / tiles;
+  static const int wg_target = [] {  // AA_BG_WG: workgroups a split k_bgemm aims at (A/B probe)
+    const char* e = getenv("AA_BG_WG");
+    return e ? atoi(e) : 256;
+  }();
+  int splits = tiles >= 512 ? 1 : (wg_target + tiles - 1) / tiles;
   if (splits > ksteps) splits = ksteps;
   const size_t capsp = gc.split ? gc.cap / ((size_t)M * N) : 1;
   if ((size_t)splits > capsp) splits = (int)capsp;
