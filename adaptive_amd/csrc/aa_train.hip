@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
     const float4 x = *reinterpret_cast<const float4*>(base), y = *reinterpret_cast<const float4*>(base + 4);
     r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w; r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
   };
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, float (&ra)[HH][8], float (&rw)[HH][8]) {
 #pragma unroll
     for (int hh = 0; hh < HH; ++hh) {
       const int kh = k0 + 32 * hh;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
       }
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, float (&ra)[HH][8], float (&rw)[HH][8]) {
 #pragma unroll
     for (int hh = 0; hh < HH; ++hh) {
       const int ko = 32 * hh;
@@ -207,12 +207,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int nk = (kend - kbeg + TBK - 1) / TBK;
-  gload(kbeg);
-  lstore(0);
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) gload(kbeg + (ks + 1) * TBK);
+  auto compute = [&](int buf) {
     if constexpr (BF) {
       const __bf16* As = reinterpret_cast<const __bf16*>(lds[buf][0]);
       const __bf16* Ws = reinterpret_cast<const __bf16*>(lds[buf][1]);
@@ -233,7 +228,16 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
         for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a, j), f4c(w, j), acc, 0, 0, 0);
       }
     }
-    if (ks + 1 < nk) lstore(buf ^ 1);
+  };
+  // (loading two K steps ahead from two register sets -- 145 VGPRs, three waves per SIMD instead of
+  // four -- was bit-identical and 1-2 % slower over the training step: profiles/r06z6_train_tgemm_pf2_ab.txt)
+  gload(kbeg, ra, rw);
+  lstore(0, ra, rw);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * TBK, ra, rw);
+    compute(ks & 1);
+    if (ks + 1 < nk) lstore((ks & 1) ^ 1, ra, rw);
     __syncthreads();
   }
   const int col = n0 + wnv * 32 + li;
