@@ -306,7 +306,7 @@ __global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* x, int64_t l
   for (; j < V; j += CE_THREADS) dr[j] = (expf(xr[j] - L) - (j == t ? 1.f : 0.f)) * scale;
 }
 
-// ---- clip_grad_norm_ (torch.nn.utils.clip_grad_norm_(params, max_norm), 2-norm; train.py:210) --------
+// ---- clip_grad_norm_ (torch.nn.utils.clip_grad_norm_(params, max_norm), 2-norm; train.py:213-214) --------
 // torch: norms = _foreach_norm(grads); total = vector_norm(stack(norms)); coef = max_norm / (total +
 // 1e-6); grads *= clamp(coef, max=1).  Here: k_clip_sumsq writes one fp32 sum of squares per workgroup
 // (CLIP_CHUNK elements of one tensor, a fixed order), k_clip_norm adds each tensor's partials in block

@@ -137,7 +137,7 @@ _clip_cache = {}
 
 def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_if_nonfinite: bool = False,
                     foreach=None) -> torch.Tensor:
-    """torch.nn.utils.clip_grad_norm_ with the 2-norm (train.py:210: ``clip_grad_norm_(lstm params,
+    """torch.nn.utils.clip_grad_norm_ with the 2-norm (train.py:213-214: ``clip_grad_norm_(lstm params,
     cf.clip)``) for fp32 contiguous GPU gradients, as one ``aa_clip_grad_norm`` host call (three
     launches per 24 tensors): per-tensor norms, the total over them, every gradient scaled in place by
     ``min(max_norm / (total + 1e-6), 1)``.  Returns the total norm as a 0-d device tensor, as torch
@@ -146,7 +146,7 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
         parameters = [parameters]
     grads = [p.grad for p in parameters if p.grad is not None]
     if float(norm_type) != 2.0:
-        raise NotImplementedError("adaptive_amd.optim.clip_grad_norm_: only the 2-norm (train.py:210)")
+        raise NotImplementedError("adaptive_amd.optim.clip_grad_norm_: only the 2-norm (train.py:213-214)")
     if not grads:
         return torch.tensor(0.0)
     dev = grads[0].device

@@ -371,7 +371,7 @@ typedef struct aa_adam_tensor {
 AA_API int aa_adam_step(const aa_adam_tensor* tensors, int32_t n, double step, double lr, double beta1,
                         double beta2, double eps, double weight_decay, aa_stream_t stream);
 
-/* aa_clip_grad_norm: torch.nn.utils.clip_grad_norm_(params, max_norm) with the 2-norm (train.py:210
+/* aa_clip_grad_norm: torch.nn.utils.clip_grad_norm_(params, max_norm) with the 2-norm (train.py:213-214
  * clips the LSTM's gradients to 5): total = sqrt(sum_i ||g_i||^2) over the tensors' norms, coef =
  * max_norm / (total + 1e-6), every gradient multiplied in place by min(coef, 1) (NaN kept); the total
  * norm is written to total_norm (a device float).  Fixed reduction order: deterministic.  Up to

@@ -203,7 +203,7 @@ def test_train_closure_with_hip_loss_and_adam(gpu_device):
 
 @pytest.mark.parametrize("max_norm", [5.0, 1e30, 0.0])
 def test_clip_grad_norm_matches_torch(gpu_device, max_norm):
-    """clip_grad_norm_ (train.py:210) vs torch.nn.utils.clip_grad_norm_: tensor sizes either side of
+    """clip_grad_norm_ (train.py:213-214) vs torch.nn.utils.clip_grad_norm_: tensor sizes either side of
     the kernel's 8192-element chunk, an empty tensor, an unaligned view, a parameter without a
     gradient; the total norm to fp32 rounding (the sum order differs), the clipped gradients to a few
     ulps (the same multiply by a coefficient that differs by at most that), and no clip due leaves the
