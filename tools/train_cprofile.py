@@ -28,12 +28,12 @@ def main():
     opt = aa_optim.Adam(model.parameters(), lr=1e-4)
     crit = aa_optim.CrossEntropyLoss()
     for _ in range(6):
-        step(model, opt, crit, feats, caps, lengths)
+        step(model, opt, crit, feats, caps, lengths, aa_optim.clip_grad_norm_)
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(40):
-        step(model, opt, crit, feats, caps, lengths)
+        step(model, opt, crit, feats, caps, lengths, aa_optim.clip_grad_norm_)
     pr.disable()
     torch.cuda.synchronize()
     st = pstats.Stats(pr)
