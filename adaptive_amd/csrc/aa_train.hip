@@ -879,7 +879,41 @@ __global__ void k_colsum_fin(const float* __restrict__ part, int N, float* __res
   for (int ch = 0; ch < CS_CH; ++ch) s += part[(int64_t)ch * N + n];
   out[n] = s;
 }
+// k_colsum + k_colsum_fin in one launch for short columns (M <= CS1_MAXM: the encoder-head bias
+// gradients over the B rows): a workgroup per 64 columns, wave g sums chunks [16 g, 16 g + 16) of
+// its lane's column (k_colsum's chunks, rows in order from 0), the 64 chunk sums go through LDS and
+// lane c of wave 0 adds them in chunk order from 0 -- k_colsum_fin's arithmetic: the same bits, one
+// launch instead of two, every load of a thread in flight at once.
+constexpr int CS1_MAXM = 512;
+__global__ __launch_bounds__(256) void k_colsum1(const float* __restrict__ X, int M, int N, int64_t ldx,
+                                                 float* __restrict__ out) {
+  __shared__ float cs[CS_CH][65];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6, n = blockIdx.x * 64 + c;
+  const int per = (M + CS_CH - 1) / CS_CH;
+  const int nc = n < N ? n : N - 1;
+  for (int j = 0; j < CS_CH / 4; ++j) {
+    const int ch = 16 * g + j, m0 = ch * per, m1 = m0 + per < M ? m0 + per : M;
+    float x[CS1_MAXM / CS_CH];
+#pragma unroll
+    for (int i = 0; i < CS1_MAXM / CS_CH; ++i) x[i] = m0 + i < m1 ? X[(int64_t)(m0 + i) * ldx + nc] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CS1_MAXM / CS_CH; ++i)
+      if (m0 + i < m1) s += x[i];
+    cs[ch][c] = s;
+  }
+  __syncthreads();
+  if (g == 0 && n < N) {
+    float s = 0.f;
+    for (int ch = 0; ch < CS_CH; ++ch) s += cs[ch][c];
+    out[n] = s;
+  }
+}
 static void colsum(hipStream_t st, const float* X, int M, int N, int64_t ldx, float* scratch, float* out) {
+  if (M > 0 && M <= CS1_MAXM) {
+    hipLaunchKernelGGL(k_colsum1, dim3((N + 63) / 64), dim3(256), 0, st, X, M, N, ldx, out);
+    return;
+  }
   hipLaunchKernelGGL(k_colsum, dim3((N + 255) / 256, CS_CH), dim3(256), 0, st, X, M, N, ldx, scratch);
   hipLaunchKernelGGL(k_colsum_fin, dim3((N + 255) / 256), dim3(256), 0, st, scratch, N, out);
 }
