@@ -310,9 +310,9 @@ __global__ __launch_bounds__(CE_THREADS) void k_ce_bwd(const float* x, int64_t l
 // torch: norms = _foreach_norm(grads); total = vector_norm(stack(norms)); coef = max_norm / (total +
 // 1e-6); grads *= clamp(coef, max=1).  Here: k_clip_sumsq writes one fp32 sum of squares per workgroup
 // (CLIP_CHUNK elements of one tensor, a fixed order), k_clip_norm adds each tensor's partials in block
-// order, takes the norm, combines the tensors' norms as torch does and writes (total, coef); k_clip_scale
-// multiplies every gradient by the clamped coefficient (a multiply by exactly 1.0 when no clip is due,
-// as torch's).  Three launches, one host call.
+// order, takes the norm, combines the tensors' norms as torch does and writes the total (the caller's
+// float) and the coefficient; k_clip_scale multiplies every gradient by the clamped coefficient (a
+// multiply by exactly 1.0 when no clip is due, as torch's).  Three launches, one host call.
 constexpr int CLIP_THREADS = 256, CLIP_VEC = 4, CLIP_ROUNDS = 8;
 constexpr int CLIP_CHUNK = CLIP_THREADS * CLIP_VEC * CLIP_ROUNDS;  // 8192 elements per workgroup
 struct ClipArgs {
@@ -322,7 +322,8 @@ struct ClipArgs {
   int64_t numel[AA_CLIP_MAX_TENSORS];
   float* g[AA_CLIP_MAX_TENSORS];
   float* part;      // [workgroups] sums of squares
-  float* out;       // [2]: total norm, clamped coefficient
+  float* out;       // [2]: (unused), clamped coefficient
+  float* total;     // the caller's total-norm float
   float max_norm;
 };
 __device__ __forceinline__ int clip_tensor(const ClipArgs& a, int64_t blk) {
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(CLIP_THREADS) void k_clip_norm(ClipArgs a) {
     for (int t = 0; t < a.n; ++t) s = fmaf(norms[t], norms[t], s);
     const float total = sqrtf(s);
     const float coef = a.max_norm / (total + 1e-6f);
-    a.out[0] = total;
+    *a.total = total;
     a.out[1] = coef > 1.f ? 1.f : coef;  // clamp(max = 1) that keeps a NaN, as torch.clamp does
   }
 }
@@ -490,14 +491,12 @@ int aa_clip_grad_norm(const aa_grad_tensor* tensors, int32_t n, float max_norm, 
   float* ws = (float*)workspace;
   a.out = ws;
   a.part = ws + 2;
+  a.total = total_norm;
   a.max_norm = max_norm;
   hipStream_t st = (hipStream_t)stream;
   if (blocks > 0) hipLaunchKernelGGL(k_clip_sumsq, dim3((unsigned)blocks), dim3(CLIP_THREADS), 0, st, a);
   hipLaunchKernelGGL(k_clip_norm, dim3(1), dim3(CLIP_THREADS), 0, st, a);
   if (blocks > 0) hipLaunchKernelGGL(k_clip_scale, dim3((unsigned)blocks), dim3(CLIP_THREADS), 0, st, a);
-  // the total norm, as torch returns it (a device scalar)
-  const hipError_t e = hipMemcpyAsync(total_norm, ws, sizeof(float), hipMemcpyDeviceToDevice, st);
-  if (e != hipSuccess) return (int)e;
   return (int)hipGetLastError();
 }
 

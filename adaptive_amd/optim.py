@@ -166,13 +166,16 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
         nbytes = lib.aa_clip_grad_norm_workspace_bytes(arr, len(grads))
         if nbytes == 0:
             raise RuntimeError("adaptive_amd.optim.clip_grad_norm_: invalid gradient table")
-        ent = (arr, torch.empty(nbytes, dtype=torch.uint8, device=dev))
+        ent = (arr, nbytes)
         if len(_clip_cache) > 16:
             _clip_cache.clear()
         _clip_cache[key] = ent
-    arr, ws = ent
+    arr, nbytes = ent
     for i, g in enumerate(grads):
         arr[i].grad = g.data_ptr()
+    # the workspace comes from the caching allocator on every call (stream-ordered: calls on
+    # different streams never share one); the launch table is copied into the kernel arguments
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     total = torch.empty((), dtype=torch.float32, device=dev)
     with torch.cuda.device(dev):
         rc = lib.aa_clip_grad_norm(arr, len(grads), float(max_norm), total.data_ptr(), ws.data_ptr(), ws.numel(),
