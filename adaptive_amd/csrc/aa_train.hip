@@ -253,6 +253,20 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
   }
   if (col >= g.N) return;
   const float bv = (g.bias ? g.bias[col] : 0.f) + (g.bias2 ? g.bias2[col] : 0.f);
+  // accumulate: the 16 old values are loaded together before any store (a load after a store to C
+  // may alias it, so loads interleaved with the stores each waited a full round trip: 16 per thread)
+  float* dst[16];
+  float old[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wmv * 32 + acc_row(r, lane);
+    const int mc = m < g.M ? m : g.M - 1;
+    dst[r] = g.C + (int64_t)(g.crow ? g.crow[mc] : mc) * g.ldc + col;
+  }
+  if (g.accumulate) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) old[r] = m0 + wmv * 32 + acc_row(r, lane) < g.M ? *dst[r] : 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = m0 + wmv * 32 + acc_row(r, lane);
@@ -260,8 +274,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TG g) {
     float v = acc[r] + bv;
     if (g.act == 1) v = reluf_(v);
     else if (g.act == 2) v = tanhf(v);
-    float* dst = g.C + (int64_t)(g.crow ? g.crow[m] : m) * g.ldc + col;
-    *dst = g.accumulate ? *dst + v : v;
+    *dst[r] = g.accumulate ? old[r] + v : v;
   }
 }
 
