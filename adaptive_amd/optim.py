@@ -48,6 +48,16 @@ class Adam(torch.optim.Optimizer):
                                       fused=None))
         self._tables = {}
 
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """torch.optim.Optimizer.zero_grad (train.py:204); set_to_none=True (the default) as one loop
+        over the groups' parameters without the profiler scope, otherwise torch's own."""
+        if not set_to_none:
+            return super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    p.grad = None
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
