@@ -768,7 +768,7 @@ class _TeacherForced(torch.autograd.Function):
         ws = torch.empty(nbytes, dtype=torch.uint8, device=images.device)
         scores = torch.empty(N, owner.dims.vocab, device=images.device)
         w = _lib.RefWeights(*[p.data_ptr() for p in params])
-        with torch.cuda.device(images.device):
+        with _lib.on_device(images.device):
             rc = lib.aa_train_forward_aux(w, d, images.data_ptr(), B, T, caps.data_ptr(), caps.stride(0),
                                           len_dev.data_ptr(), scores.data_ptr(), N, ws.data_ptr(), nbytes,
                                           owner._train_flags(), _lib.stream_handle(), owner._train_aux(images.device))
@@ -788,7 +788,7 @@ class _TeacherForced(torch.autograd.Function):
         dfeats = torch.empty_like(images) if ctx.needs_input_grad[1] else None
         w = _lib.RefWeights(*[p.data_ptr() for p in params])
         g = _lib.RefWeights(*[t.data_ptr() for t in grads])
-        with torch.cuda.device(images.device):
+        with _lib.on_device(images.device):
             rc = lib.aa_train_backward_aux(w, owner._c_dims(), images.data_ptr(), B, ctx.T, caps.data_ptr(),
                                            caps.stride(0), len_dev.data_ptr(), dscores.data_ptr(), ctx.N, g,
                                            _lib.ptr(dfeats), ctx.ws.data_ptr(), ctx.ws.numel(), ctx.flags,

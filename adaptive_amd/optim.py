@@ -94,7 +94,7 @@ class Adam(torch.optim.Optimizer):
             sbuf.add_(1.0)
             for dev, first, arr, n in calls:
                 step = float(sbuf[first].item())
-                with torch.cuda.device(dev):
+                with _lib.on_device(dev):
                     rc = lib.aa_adam_step(arr, n, step, group["lr"], beta1, beta2, group["eps"],
                                           group["weight_decay"], _lib.stream_handle())
                 _lib.check(rc, "adam_step")
@@ -187,7 +187,7 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     # different streams never share one); the launch table is copied into the kernel arguments
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     total = torch.empty((), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         rc = lib.aa_clip_grad_norm(arr, len(grads), float(max_norm), total.data_ptr(), ws.data_ptr(), ws.numel(),
                                    _lib.stream_handle())
     _lib.check(rc, "clip_grad_norm")
@@ -206,7 +206,7 @@ class _CrossEntropy(torch.autograd.Function):
         ws = torch.empty(lib.aa_cross_entropy_workspace_bytes(N), dtype=torch.uint8, device=x.device)
         loss = torch.empty((), dtype=torch.float32, device=x.device)
         count = torch.empty(1, dtype=torch.float32, device=x.device)
-        with torch.cuda.device(x.device):
+        with _lib.on_device(x.device):
             rc = lib.aa_cross_entropy_forward(x.data_ptr(), N, V, x.stride(0), target.data_ptr(), ignore_index,
                                               loss.data_ptr(), count.data_ptr(), ws.data_ptr(), ws.numel(),
                                               _lib.stream_handle())
@@ -222,7 +222,7 @@ class _CrossEntropy(torch.autograd.Function):
         N, V = x.shape
         dloss = dloss.contiguous().float()
         dx = torch.empty(N, V, dtype=torch.float32, device=x.device)
-        with torch.cuda.device(x.device):
+        with _lib.on_device(x.device):
             rc = lib.aa_cross_entropy_backward(x.data_ptr(), N, V, x.stride(0), target.data_ptr(), ctx.ignore_index,
                                                dloss.data_ptr(), count.data_ptr(), ws.data_ptr(), ws.numel(),
                                                dx.data_ptr(), dx.stride(0), _lib.stream_handle())

@@ -48,6 +48,11 @@ def test_fresh_images_per_call_with_trunk(gpu_device):
     g = torch.Generator().manual_seed(0)
     imgs = [torch.rand(6, 3, 224, 224, generator=g) for _ in range(2)]
     with torch.no_grad():
+        # one untimed call first: MIOpen may pick the trunk's convolution algorithms on the first call
+        # of a shape and switch to the tuned ones after it (different rounding in the random-init
+        # trunk's features: the alphas moved by up to 2e-2 between those calls on one box)
+        for im in imgs:
+            m.sampler(im.to(gpu_device), max_len=8)
         ref = [m.sampler(im.to(gpu_device), max_len=8) for im in imgs]
     captures0 = Encoder2Decoder._captures
     for i in range(8):
